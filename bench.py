@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark: validated candidates/s of the MI355X validator on the force-free depth-4 batch.
+
+Workload (BASELINE.json configs[2], "force_free --max-depth 4 on 1xMI355X"):
+the candidates of the reference's depth-4 force-free stream (tests/golden/streams, compiled
+into data/force_free_d4_*.npz), tiled and shuffled with seed 0 into a batch of --n candidates
+per GPU.  One "step" = one validation pass of the whole batch: every candidate's program is
+evaluated in jets at the reference point and on the 64x64 (rho, z) grid (4097 points), the
+foliation determinant and its scaled zero test are applied and the verdict bitmap + per-
+candidate outputs are written to HBM.  Inputs are resident in HBM before timing starts.
+
+Multi-GPU (torchrun, one process per GPU): each rank validates its own contiguous shard
+(weak scaling, no data-path collective); after timing, one RCCL all-gather of the verdict
+bitmaps assembles the global result on every rank.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'pde-engine_amd'))
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
+
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (spec; MI355X_MICROARCH.md lists FP32 157.3 = 2x)
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s"
+
+
+def load_workload(problem):
+    for name in (f'{problem}_d4_validated.npz', f'{problem}_d4_stream.npz'):
+        p = os.path.join(ROOT, 'data', name)
+        if os.path.exists(p):
+            z = np.load(p, allow_pickle=False)
+            return name, z['ops'], z['offsets']
+    raise FileNotFoundError('data/*_d4_*.npz missing')
+
+
+def gather_programs(ops, offsets, idx):
+    """Batch of programs idx[...] (contiguous, in order) from a program table."""
+    lens = (offsets[idx + 1] - offsets[idx]).astype(np.int64)
+    new_off = np.zeros(len(idx) + 1, dtype=np.int64)
+    np.cumsum(lens, out=new_off[1:])
+    starts = np.repeat(offsets[idx], lens)
+    within = np.arange(new_off[-1], dtype=np.int64) - np.repeat(new_off[:-1], lens)
+    return ops[starts + within], new_off
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--n', type=int, default=1 << 20, help='candidates per GPU per step')
+    ap.add_argument('--problem', default='force_free')
+    ap.add_argument('--early-exit', action='store_true',
+                    help='stop after the point stage for point-rejects (the reference\'s control flow)')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0, help='CPU-baseline time budget')
+    ap.add_argument('--no-cpu', action='store_true')
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from pdeval import _lib
+    from pdeval.opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR, FP_N
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device(f'cuda:{local}'))
+    torch.cuda.set_device(local)
+    dev = torch.device(f'cuda:{local}')
+    pid = PROBLEM_FORCE_FREE if a.problem == 'force_free' else PROBLEM_KERR
+
+    wname, ops_all, off_all = load_workload(a.problem)
+    nprog = len(off_all) - 1
+    total = a.n * world
+    rng = np.random.default_rng(0)
+    tiled = np.tile(np.arange(nprog, dtype=np.int64), (total + nprog - 1) // nprog)[:total]
+    rng.shuffle(tiled)
+    idx = tiled[rank * a.n:(rank + 1) * a.n]
+    ops, off = gather_programs(ops_all, off_all, idx)
+
+    # algorithmic work of the batch (DESIGN.md "Roofline")
+    lib = _lib.load()
+    flops_prog = np.array([lib.pdeval_program_flops(pid, ops_all[off_all[i]:].ctypes.data,
+                                                    int(off_all[i + 1] - off_all[i]))
+                           for i in range(nprog)])
+    ctx = _lib.Context(pid, device=local)
+    npts, nref = ctx.n_points, ctx.n_ref
+    flops_step = float(flops_prog[idx].sum()) * npts
+    out_bytes_per = 1 + 8 + 8 * nref + 8 + 4 + 4 + 8 * FP_N + 1.0 / 8
+    bytes_step = ops.nbytes + off.nbytes + a.n * out_bytes_per
+
+    d_ops = torch.from_numpy(ops).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    n = a.n
+    outs = dict(verdict_bits=torch.zeros(((n + 31) // 32) * 4, dtype=torch.uint8, device=dev),
+                status=torch.zeros(n, dtype=torch.uint8, device=dev),
+                q_ref=torch.zeros(n, dtype=torch.float64, device=dev),
+                res_ref=torch.zeros(n * nref, dtype=torch.float64, device=dev),
+                q_grid=torch.zeros(n, dtype=torch.float64, device=dev),
+                n_bad=torch.zeros(n, dtype=torch.int32, device=dev),
+                n_nonfinite=torch.zeros(n, dtype=torch.int32, device=dev),
+                fingerprint=torch.zeros(n * FP_N, dtype=torch.float64, device=dev))
+    d_out = _lib.Outputs(*[outs[f].data_ptr() for f, _ in _lib.Outputs._fields_])
+    prm = _lib.default_params(pid)
+    prm.full_grid = 0 if a.early_exit else 1
+    # all uploads / zero-fills above ran on torch's default stream: finish them, then run the
+    # hot path on a dedicated stream that the events below are recorded on
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.Stream(dev)
+
+    def step():
+        ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out,
+                            params=prm, stream=stream.cuda_stream, zero_bits=True)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        step()
+        e.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    # the one exchange step: all-gather of the verdict bitmaps over RCCL
+    bits = outs['verdict_bits']
+    if world > 1:
+        allbits = torch.empty(world * bits.numel(), dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(allbits, bits)
+    else:
+        allbits = bits
+    status = outs['status'].cpu().numpy()
+    n_acc_local = int(np.unpackbits(bits.cpu().numpy(), bitorder='little')[:n].sum())
+
+    if rank == 0:
+        value = total * a.steps / elapsed
+        achieved_tf = flops_step / (kern_ms * 1e-3) / 1e12
+        achieved_gbs = bytes_step / (kern_ms * 1e-3) / 1e9
+        res = {
+            'metric': 'validated candidates/sec (force-free depth-4 batch, 64x64 grid + p*)',
+            'value': value, 'unit': 'candidates/s', 'n_gpus': world, 'steps': a.steps,
+            'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
+            'config': {'workload': f'{a.problem} depth-4 candidates ({wname}, {nprog} programs) '
+                                   f'tiled+shuffled(seed 0) to {a.n}/GPU; 64x64 grid + ref point',
+                       'problem': a.problem, 'candidates_per_gpu': a.n, 'points_per_candidate': npts,
+                       'full_grid': not a.early_exit, 'parallelism': f'shard{world}'},
+            'roofline': {'bound': 'valu_fp64', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
+                         'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': None,
+                         'kernel_ms': kern_ms, 'flops_per_step': flops_step},
+            'roofline_hbm': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
+                             'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
+                             'bytes_per_step': bytes_step},
+            'accepted_local': n_acc_local,
+            'status_hist': np.bincount(status, minlength=7).tolist(),
+        }
+        if not a.no_cpu and world == 1:
+            res['cpu_baseline'] = cpu_baseline(pid, ops_all, off_all, idx, a.cpu_seconds)
+        print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pid, ops_all, off_all, idx, budget_s):
+    """The C oracle (a CPU port of the same validation) on a bounded sample of the same
+    workload, one core."""
+    import oracle_lib as O
+    sample = idx[:4096]
+    ops, off = gather_programs(ops_all, off_all, sample)
+    done, t0 = 0, time.perf_counter()
+    while done < len(sample) and time.perf_counter() - t0 < budget_s:
+        O.validate(pid, ops, off, first=done, count=64)
+        done += 64
+    dt = time.perf_counter() - t0
+    return {'value': done / dt, 'unit': 'candidates/s', 'cores': 1, 'kind': 'port',
+            'sample': f'first {done} candidates of this batch (same 4097 points each), '
+                      f'C oracle oracle/jet_oracle.c, 1 thread, {dt:.1f}s'}
+
+
+if __name__ == '__main__':
+    main()

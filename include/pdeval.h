@@ -1,0 +1,158 @@
+/*
+ * pdeval.h -- C ABI of libpdeval.so, the MI355X (gfx950) candidate validator.
+ *
+ * Drop-in boundary for the per-candidate PDE-residual check of PimDeWitte/pde-engine.
+ * One call validates a whole batch of candidate expressions; it replaces, per candidate,
+ *   - problems/force_free/validator.py:260-437           PreciseFoliationValidator.validate
+ *   - problems/kerr_magnetosphere/validator.py:210-345   KerrMagnetosphereValidator.validate
+ * as called by the validator worker pool (general_method_paper_reproduction.py:1671-1824,
+ * the per-candidate loop :1753-1812) and by the inline path (:1288-1339).  The reference has
+ * no native code and no FFI; the Python side of this boundary (ctypes) lives in
+ * pde-engine_amd/pdeval/_lib.py and is the "binding a maintainer would add" (INTEGRATION.md).
+ *
+ * Conventions: plain C, no exceptions cross the boundary, every entry point returns an int
+ * status (PDEVAL_OK = 0), caller-owned host buffers, library-owned device buffers and HIP
+ * stream, one context per GPU, calls on one context serialized by the caller.
+ *
+ * Candidate programs (the flattened SymPy tree, see DESIGN.md "Program format"):
+ *   ops      int32 words of ALL programs, concatenated; program i is ops[offsets[i] ..
+ *            offsets[i+1]).  Word = opcode (bits 0-7) | small operand (bits 8-31); opcodes
+ *            that carry an f64 immediate are followed by two words holding its IEEE bits
+ *            (low word first).
+ *   offsets  int64[n+1], offsets[0] = 0, non-decreasing.
+ */
+#ifndef PDEVAL_H
+#define PDEVAL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes returned by every entry point ---- */
+#define PDEVAL_OK              0
+#define PDEVAL_ERR_ARG         1   /* bad argument (null ctx, n < 0, bad offsets ...) */
+#define PDEVAL_ERR_HIP         2   /* a HIP runtime call failed; see pdeval_last_error */
+#define PDEVAL_ERR_PROGRAM     3   /* a program failed host-side validation */
+#define PDEVAL_ERR_NODEVICE    4
+
+/* ---- problems (the problems/ plugin registry, problems/__init__.py:355-361) ---- */
+#define PDEVAL_PROBLEM_FORCE_FREE   0   /* foliation determinant, jets of order 4 */
+#define PDEVAL_PROBLEM_KERR         1   /* Kerr linear surrogate, jets of order 2 */
+
+/* ---- per-candidate class (status[] output) ---- */
+#define PDEVAL_CLS_ACCEPT          0   /* residual ~ 0 at the reference point(s) and on the grid */
+#define PDEVAL_CLS_REJECT_POINT    1   /* rejected by the reference-point stage            */
+#define PDEVAL_CLS_REJECT_GRID     2   /* passed the point stage, residual != 0 on the grid */
+#define PDEVAL_CLS_ZERO_GRADIENT   3   /* u is constant (force-free :309-312, Kerr :231-240) */
+#define PDEVAL_CLS_NONFINITE_REF   4   /* non-finite at a reference point in real arithmetic */
+#define PDEVAL_CLS_UNSUPPORTED     5   /* program uses an opcode this build does not handle */
+#define PDEVAL_CLS_BAD_PROGRAM     6   /* malformed program (stack under/overflow)          */
+
+/* ---- opcodes (bits 0-7 of a program word) ---- */
+enum pdeval_opcode {
+    PDOP_PUSH_X   = 1,   /* push coordinate 1 (rho | r)                          */
+    PDOP_PUSH_Y   = 2,   /* push coordinate 2 (z | x)                            */
+    PDOP_PUSH_C   = 3,   /* push constant            [f64 imm]                   */
+    PDOP_ADD      = 4,   /* b=pop, a=pop, push a+b                               */
+    PDOP_SUB      = 5,   /* a-b                                                  */
+    PDOP_RSUB     = 6,   /* b-a                                                  */
+    PDOP_MUL      = 7,   /* a*b                                                  */
+    PDOP_DIV      = 8,   /* a/b                                                  */
+    PDOP_RDIV     = 9,   /* b/a                                                  */
+    PDOP_ADDC     = 10,  /* top += c                 [f64 imm]                   */
+    PDOP_MULC     = 11,  /* top *= c                 [f64 imm]                   */
+    PDOP_RDIVC    = 12,  /* top = c / top            [f64 imm]                   */
+    PDOP_NEG      = 13,  /* top = -top                                           */
+    PDOP_ADD_X    = 14,  /* top += x                                             */
+    PDOP_ADD_Y    = 15,  /* top += y                                             */
+    PDOP_MUL_X    = 16,  /* top *= x                                             */
+    PDOP_MUL_Y    = 17,  /* top *= y                                             */
+    PDOP_SUB_X    = 18,  /* top -= x                                             */
+    PDOP_SUB_Y    = 19,  /* top -= y                                             */
+    PDOP_POWN     = 20,  /* top = top**n, n = operand bits 8-15, 2 <= n <= 16    */
+    PDOP_POW      = 21,  /* top = top**alpha (principal branch) [f64 imm alpha]  */
+    PDOP_EXP      = 22,
+    PDOP_LOG      = 23,
+    PDOP_ABS      = 24,
+    PDOP_SQRT     = 25,  /* = POW 1/2, kept separate (common, cheaper x0**alpha) */
+    PDOP_DIV_X    = 26,  /* top /= x                                             */
+    PDOP_DIV_Y    = 27,  /* top /= y                                             */
+    PDOP_PUSH_I   = 28,  /* push the imaginary unit (complex pass only)          */
+    PDOP_COUNT_   = 29,
+    PDOP_UNSUPPORTED = 254  /* placeholder for a construct the flattener cannot lower;
+                               the candidate is classified PDEVAL_CLS_UNSUPPORTED       */
+};
+
+#define PDEVAL_MAX_STACK  8   /* deepest program stack any kernel variant accepts */
+
+/* Program header word: opcode 0 | stack depth << 8 | flags */
+#define PDEVAL_FLAG_COMPLEX  (1u << 16)  /* pushes the imaginary unit: complex pass only   */
+#define PDEVAL_FLAG_NOCOORD  (1u << 17)  /* references no coordinate (u is a constant)   */
+
+/* Thresholds of the scaled zero test (DESIGN.md "Zero test"). */
+typedef struct pdeval_params {
+    double tau_point;    /* point stage: reject iff q* > tau_point                 */
+    double tau_grid;     /* grid stage: a finite grid point is "bad" iff q > tau_grid */
+    double kerr_abs_tol; /* Kerr fast point check: reject iff max|lhs| >= this (1e-10) */
+    int32_t full_grid;   /* 1: evaluate the whole grid for every candidate;
+                            0: stop after the point stage for point-rejects (as the
+                               reference does, validator.py:371-402)                 */
+    int32_t max_bad;     /* grid stage rejects iff n_bad > max_bad                   */
+} pdeval_params;
+
+/* Per-candidate outputs; any pointer may be NULL (not produced).  Host or device memory
+ * depending on the entry point.  n_ref = pdeval_n_ref_points(ctx).                    */
+typedef struct pdeval_outputs {
+    uint8_t* verdict_bits;   /* ceil(n/8) bytes, bit i = candidate i accepted (LSB first) */
+    uint8_t* status;         /* n, PDEVAL_CLS_*                                            */
+    double*  q_ref;          /* n, scaled residual at the point stage (Kerr: max |lhs|)    */
+    double*  res_ref;        /* n * n_ref, raw residual at each reference point            */
+    double*  q_grid;         /* n, max scaled residual over the finite grid points         */
+    int32_t* n_bad;          /* n, grid points with q > tau_grid                           */
+    int32_t* n_nonfinite;    /* n, grid points where the evaluation was not finite         */
+    double*  fingerprint;    /* n * PDEVAL_FP_N, u at fixed points (known-solution tags)   */
+} pdeval_outputs;
+
+#define PDEVAL_FP_N 4
+
+typedef struct pdeval_ctx pdeval_ctx;
+
+/* grid: {x_lo, x_hi, nx, y_lo, y_hi, ny, x_phase, y_phase}; NULL = the problem's default
+ * grid (DESIGN.md "Grids").  Point i of axis x is x_lo + (i + x_phase) * (x_hi-x_lo)/nx. */
+int pdeval_create(int device_id, int problem_id, const double* grid, int n_grid, pdeval_ctx** out);
+int pdeval_destroy(pdeval_ctx* ctx);
+const char* pdeval_last_error(pdeval_ctx* ctx);
+
+int pdeval_n_ref_points(pdeval_ctx* ctx);
+int pdeval_n_points(pdeval_ctx* ctx);          /* n_ref + grid points */
+int pdeval_default_params(int problem_id, pdeval_params* out);
+
+/* Host pointers in and out: upload, validate, download (synchronous). */
+int pdeval_validate_batch(pdeval_ctx* ctx, const int32_t* ops, int64_t n_words,
+                          const int64_t* offsets, int64_t n, const pdeval_params* params,
+                          pdeval_outputs* out);
+
+/* Device pointers in and out, asynchronous on `stream` (a hipStream_t; NULL = the
+ * context's own non-blocking stream, which does NOT wait for work on the legacy null
+ * stream: the caller must have made the inputs ready on it).  Inputs already resident in
+ * HBM: this is the timed hot path.  verdict_bits must hold ceil(n/32)*4 bytes, 4-byte
+ * aligned, zeroed by the caller or by passing zero_bits = 1.  Programs whose offsets fall
+ * outside [0, n_words] are classified PDEVAL_CLS_BAD_PROGRAM, never dereferenced.       */
+int pdeval_validate_device(pdeval_ctx* ctx, const int32_t* d_ops, int64_t n_words,
+                           const int64_t* d_offsets, int64_t n, const pdeval_params* params,
+                           const pdeval_outputs* d_out, void* stream, int zero_bits);
+
+/* Host-side program analysis (no GPU): required stack depth, or < 0 if malformed.      */
+int pdeval_program_depth(const int32_t* ops, int64_t n_words);
+
+/* Algorithmic cost model: FP64 flops per grid point for one program.      */
+double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words);
+
+const char* pdeval_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDEVAL_H */

@@ -1,0 +1,224 @@
+/* jet_oracle.c -- CPU restatement of the candidate validator (TEST INFRASTRUCTURE ONLY).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this library,
+ * and only as the checker / the timed CPU baseline -- the product path (libpdeval.so) never
+ * links or calls it.
+ *
+ * What it restates (all citations into /root/reference):
+ *   force-free  problems/force_free/validator.py:260-402 -- derivatives of u (:305-320),
+ *               A, B (:323-324, Omega = 0 on the problem path :82-83), the Lie derivative
+ *               L_T f = u_z f_rho - u_rho f_z (:335-339), det (:347), the point stage at
+ *               (rho, z) = (4/5, 6/7) (:296-297, :349-402) and the zero-gradient exit (:309-312);
+ *               the symbolic stage (:404-427) is restated as "zero at every finite grid point".
+ *   Kerr        problems/kerr_magnetosphere/validator.py:69-91 (operator), :163-192 (3-point
+ *               check, absolute 1e-10), :231-240 (constant exclusion), :283-315 (exact zero).
+ * Numerics: double jets for the real pass, double complex for the complex (principal branch)
+ * pass; the determinant is written out in closed form in the partials u_ij rather than by
+ * jets (the device does the latter), so device and oracle agree only if both are right.
+ */
+#include <complex.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/pdeval.h"
+
+#define KMAX 4
+#define NCMAX 15
+#define NC(K) (((K) + 1) * ((K) + 2) / 2)
+#define IDX(i, j) (((i) + (j)) * ((i) + (j) + 1) / 2 + (j))
+
+#define S double
+#define FN(name) name##_r
+#include "jet_oracle_impl.h"
+#undef S
+#undef FN
+#define S double complex
+#define FN(name) name##_c
+#include "jet_oracle_impl.h"
+#undef S
+#undef FN
+
+/* ---------------------------------------------------------------- sample points */
+/* Restates DESIGN.md "Grids" (the device builds the same table in pdeval_create). */
+static int build_points(int problem, double** px, double** py, int* n_ref) {
+    const int nx = 64, ny = 64;
+    double x_lo, x_hi, y_lo = -2.0, y_hi = 2.0, ph_x = 0.37, ph_y = 0.41;
+    int nr;
+    double rx[3], ry[3];
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+        x_lo = 0.05; x_hi = 3.0;
+        nr = 1; rx[0] = 4.0 / 5.0; ry[0] = 6.0 / 7.0;
+    } else {
+        double rp = 1.0 + sqrt(1.0 - 0.01);
+        x_lo = rp + 0.1; x_hi = rp + 6.1; y_lo = -0.98; y_hi = 0.98;
+        nr = 3;
+        rx[0] = 5.0 / 2.0; ry[0] = 3.0 / 5.0;
+        rx[1] = 7.0 / 3.0; ry[1] = 1.0 / 3.0;
+        rx[2] = 5.0;       ry[2] = -2.0 / 5.0;
+    }
+    int n = nr + nx * ny;
+    *px = (double*)malloc(sizeof(double) * n);
+    *py = (double*)malloc(sizeof(double) * n);
+    for (int k = 0; k < nr; ++k) { (*px)[k] = rx[k]; (*py)[k] = ry[k]; }
+    for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < ny; ++j) {
+            (*px)[nr + i * ny + j] = x_lo + (i + ph_x) * ((x_hi - x_lo) / nx);
+            (*py)[nr + i * ny + j] = y_lo + (j + ph_y) * ((y_hi - y_lo) / ny);
+        }
+    *n_ref = nr;
+    return n;
+}
+
+/* Kerr linear surrogate at M = 1, a = 1/10, expanded by hand from kerr validator.py:77-91:
+ * d_r[G/(1-x^2) u_r] + d_x[G/Delta u_x]
+ *   = G/(1-x^2) u_rr + G_r/(1-x^2) u_r + G/Delta u_xx + G_x/Delta u_x            */
+static void kerr_terms(double r, double x, const double complex* c, int cplx, double complex* L,
+                       double* scale) {
+    const double M = 1.0, a = 0.1;
+    double s = r * r + a * a * x * x;
+    double G = 1.0 - 2.0 * M * r / s;
+    double Gr = -2.0 * M / s + 4.0 * M * r * r / (s * s);
+    double Gx = 4.0 * M * r * a * a * x / (s * s);
+    double D = r * r - 2.0 * M * r + a * a, w = 1.0 - x * x;
+    double complex urr = 2.0 * c[IDX(2, 0)], uxx = 2.0 * c[IDX(0, 2)], ur = c[IDX(1, 0)], ux = c[IDX(0, 1)];
+    double complex t[4] = {G / w * urr, Gr / w * ur, G / D * uxx, Gx / D * ux};
+    (void)cplx;
+    *L = t[0] + t[1] + t[2] + t[3];
+    *scale = cabs(t[0]) + cabs(t[1]) + cabs(t[2]) + cabs(t[3]);
+}
+
+typedef struct {
+    double res_abs, res_re, scale;
+    int finite, grad_zero;
+    double u0;
+} pt_result;
+
+static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x, double y, int cplx,
+                            int* rc) {
+    pt_result r = {0};
+    const int K = problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    double complex cc[NCMAX];
+    if (cplx) {
+        *rc = run_c(w, nw, x, y, K, 1, cc);
+    } else {
+        double cr[NCMAX];
+        *rc = run_r(w, nw, x, y, K, 0, cr);
+        for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
+    }
+    if (*rc) return r;
+    int fin = 1;
+    for (int i = 0; i < NC(K); ++i) fin = fin && isfinite(creal(cc[i])) && isfinite(cimag(cc[i]));
+    double complex res;
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+        res = ff_det_c(cc, x, 0);
+        r.scale = creal(ff_det_c(cc, x, 1));
+    } else {
+        kerr_terms(x, y, cc, cplx, &res, &r.scale);
+    }
+    r.res_abs = cabs(res);
+    r.res_re = creal(res);
+    r.finite = fin && isfinite(creal(res)) && isfinite(cimag(res)) && isfinite(r.scale);
+    r.grad_zero = cc[IDX(1, 0)] == 0 && cc[IDX(0, 1)] == 0;
+    r.u0 = creal(cc[0]);
+    return r;
+}
+
+static double scaled(double a, double s) { return s > 0 ? a / s : (a == 0 ? 0 : INFINITY); }
+
+/* Validate n programs; outputs as in pdeval_outputs (host arrays, any may be NULL).
+ * Returns 0.  Candidate classes follow include/pdeval.h. */
+int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int64_t n,
+                    const pdeval_params* prm, uint8_t* status, double* q_ref, double* res_ref,
+                    double* q_grid, int32_t* n_bad, int32_t* n_nonfinite, double* fingerprint,
+                    int64_t first, int64_t count) {
+    double *px, *py;
+    int nref;
+    int npts = build_points(problem, &px, &py, &nref);
+    int G = npts - nref;
+    int fp[PDEVAL_FP_N] = {0};
+    for (int f = 1; f < PDEVAL_FP_N; ++f) fp[f] = nref + (int)((int64_t)G * f / PDEVAL_FP_N) + 7;
+    int64_t last = (count < 0 || first + count > n) ? n : first + count;
+    for (int64_t ci = first; ci < last; ++ci) {
+        const int32_t* w = ops + offsets[ci];
+        int64_t nw = offsets[ci + 1] - offsets[ci];
+        int cls = -1, cplx = 0;
+        double qr = 0, qmax = 0;
+        int nb = 0, nnf = 0, nfin = 0, any_grad = 0, point_reject = 0;
+        if (nw < 2 || (w[0] & 0xff) != 0) cls = PDEVAL_CLS_BAD_PROGRAM;
+        const uint32_t hdr = nw > 0 ? (uint32_t)w[0] : 0u;
+        if (cls < 0 && (hdr & PDEVAL_FLAG_COMPLEX)) {
+            if (problem == PDEVAL_PROBLEM_FORCE_FREE) cplx = 1;   /* complex-valued u */
+            else cls = PDEVAL_CLS_REJECT_POINT;                   /* Kerr: non-real at a test point */
+        }
+    again:
+        qr = 0; qmax = 0; nb = nnf = nfin = any_grad = point_reject = 0;
+        for (int p = 0; p < npts && cls < 0; ++p) {
+            int rc;
+            pt_result r = eval_point(problem, w, nw, px[p], py[p], cplx, &rc);
+            if (rc == -2 || rc == -3) { cls = PDEVAL_CLS_UNSUPPORTED; break; }
+            if (rc) { cls = PDEVAL_CLS_BAD_PROGRAM; break; }
+            for (int f = 0; f < PDEVAL_FP_N; ++f)
+                if (p == fp[f] && fingerprint) fingerprint[ci * PDEVAL_FP_N + f] = r.u0;
+            if (p < nref) {
+                if (res_ref) res_ref[ci * nref + p] = r.res_re;
+                if (r.finite && !r.grad_zero) any_grad = 1;
+                double v = problem == PDEVAL_PROBLEM_FORCE_FREE ? scaled(r.res_abs, r.scale) : r.res_abs;
+                if (!r.finite) {
+                    if (problem == PDEVAL_PROBLEM_FORCE_FREE && !cplx) { cplx = 1; goto again; }
+                    point_reject = 1;
+                } else if (!(qr >= v)) {
+                    qr = v;
+                }
+                if (p == nref - 1) {
+                    if (problem == PDEVAL_PROBLEM_FORCE_FREE) point_reject = point_reject || !(qr <= prm->tau_point);
+                    else point_reject = point_reject || !(qr < prm->kerr_abs_tol);
+                    if (point_reject && !prm->full_grid) cls = PDEVAL_CLS_REJECT_POINT;
+                }
+                continue;
+            }
+            if (r.finite) {
+                double q = scaled(r.res_abs, r.scale);
+                ++nfin;
+                if (q > qmax) qmax = q;
+                if (q > prm->tau_grid) ++nb;
+                if (!r.grad_zero) any_grad = 1;
+            } else {
+                ++nnf;
+            }
+        }
+        if (cls < 0) {
+            int structural = problem != PDEVAL_PROBLEM_FORCE_FREE || (hdr & PDEVAL_FLAG_NOCOORD);
+            if (!any_grad && nfin > 0 && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+            else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;
+            else if (nb > prm->max_bad) cls = PDEVAL_CLS_REJECT_GRID;
+            else cls = PDEVAL_CLS_ACCEPT;
+        }
+        if (status) status[ci] = (uint8_t)cls;
+        if (q_ref) q_ref[ci] = qr;
+        if (q_grid) q_grid[ci] = qmax;
+        if (n_bad) n_bad[ci] = nb;
+        if (n_nonfinite) n_nonfinite[ci] = nnf;
+    }
+    free(px);
+    free(py);
+    return 0;
+}
+
+/* u and its Taylor jet at one point (for unit tests). */
+int oracle_jet(int problem, const int32_t* w, int64_t nw, double x, double y, int cplx, double* re,
+               double* im) {
+    const int K = problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    double complex cc[NCMAX];
+    int rc;
+    if (cplx) {
+        rc = run_c(w, nw, x, y, K, 1, cc);
+    } else {
+        double cr[NCMAX];
+        rc = run_r(w, nw, x, y, K, 0, cr);
+        for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
+    }
+    for (int i = 0; i < NC(K) && !rc; ++i) { re[i] = creal(cc[i]); im[i] = cimag(cc[i]); }
+    return rc;
+}

@@ -1,0 +1,208 @@
+/* jet_oracle_impl.h -- scalar-type-generic part of the CPU oracle (included twice by
+ * jet_oracle.c: once with S = double for the real pass, once with S = double complex for the
+ * complex pass).  TEST INFRASTRUCTURE ONLY: never linked into libpdeval.
+ *
+ * Derivatives are taken by truncated bivariate Taylor arithmetic (the same mathematics as
+ * sp.diff in problems/force_free/validator.py:305-344, evaluated at a point instead of
+ * symbolically); the residual operators are then written out as CLOSED FORMS in the partial
+ * derivatives u_ij (not as jets, as the device epilogue does), so the oracle checks the
+ * device's epilogue as well as its interpreter.
+ */
+
+/* ---------- jets: c[IDX(i,j)], i + j <= KMAX, degree-major ---------- */
+static void FN(jconst)(S* t, S v) { for (int i = 0; i < NCMAX; ++i) t[i] = 0; t[0] = v; }
+
+static void FN(jmul)(const S* a, const S* b, S* c, int K) {
+    S r[NCMAX];
+    for (int d = 0; d <= K; ++d)
+        for (int j = 0; j <= d; ++j) {
+            S s = 0;
+            for (int d1 = 0; d1 <= d; ++d1)
+                for (int j1 = 0; j1 <= d1; ++j1) {
+                    int d2 = d - d1, j2 = j - j1;
+                    if (j2 < 0 || j2 > d2) continue;
+                    s += a[IDX(d1 - j1, j1)] * b[IDX(d2 - j2, j2)];
+                }
+            r[IDX(d - j, j)] = s;
+        }
+    memcpy(c, r, sizeof(S) * NC(K));
+}
+
+static void FN(jdiv)(const S* a, const S* b, S* c, int K) {  /* c = a / b */
+    S r[NCMAX];
+    for (int d = 0; d <= K; ++d)
+        for (int j = 0; j <= d; ++j) {
+            S s = a[IDX(d - j, j)];
+            for (int d1 = 1; d1 <= d; ++d1)
+                for (int j1 = 0; j1 <= d1; ++j1) {
+                    int d2 = d - d1, j2 = j - j1;
+                    if (j2 < 0 || j2 > d2) continue;
+                    s -= b[IDX(d1 - j1, j1)] * r[IDX(d2 - j2, j2)];
+                }
+            r[IDX(d - j, j)] = s / b[0];
+        }
+    memcpy(c, r, sizeof(S) * NC(K));
+}
+
+/* x <- f(x) for f with Taylor coefficients f[0..K] at x[0]: sum_k f_k h^k, h = x - x0,
+ * by explicit powers of h (the device uses Horner: a different evaluation order) */
+static void FN(jcompose)(S* x, const S* f, int K) {
+    S h[NCMAX], hk[NCMAX], acc[NCMAX];
+    memcpy(h, x, sizeof(S) * NC(K));
+    h[0] = 0;
+    FN(jconst)(acc, f[0]);
+    FN(jconst)(hk, 1);
+    for (int k = 1; k <= K; ++k) {
+        FN(jmul)(hk, h, hk, K);
+        for (int i = 0; i < NC(K); ++i) acc[i] += f[k] * hk[i];
+    }
+    memcpy(x, acc, sizeof(S) * NC(K));
+}
+
+/* principal-branch x0**alpha, with the real pass undefined off the real domain */
+static S FN(spow)(S x, double a, int cplx_pass) {
+    if (!cplx_pass) {
+        double xr = creal(x);
+        if (a == floor(a)) return pow(xr, a);
+        if (xr < 0) return NAN;
+        return pow(xr, a);
+    }
+    if (x == 0) return a > 0 ? 0 : INFINITY;
+    return cexp(a * clog(x));
+}
+
+static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, int cplx_pass, S* out) {
+    S st[16][NCMAX];
+    int d = 0;
+    for (int64_t pc = 1; pc < nw;) {
+        uint32_t word = (uint32_t)w[pc], op = word & 0xffu;
+        double imm = 0;
+        if (op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC || op == PDOP_POW) {
+            if (pc + 2 >= nw + 1) return -1;
+            uint64_t bits = (uint64_t)(uint32_t)w[pc + 1] | ((uint64_t)(uint32_t)w[pc + 2] << 32);
+            memcpy(&imm, &bits, 8);
+            pc += 3;
+        } else {
+            pc += 1;
+        }
+        S* t = d > 0 ? st[d - 1] : NULL;
+        S* u = d > 1 ? st[d - 2] : NULL;
+        S f[KMAX + 1];
+        switch (op) {
+            case PDOP_PUSH_X: FN(jconst)(st[d], px); st[d][IDX(1, 0)] = 1; ++d; break;
+            case PDOP_PUSH_Y: FN(jconst)(st[d], py); st[d][IDX(0, 1)] = 1; ++d; break;
+            case PDOP_PUSH_C: FN(jconst)(st[d], imm); ++d; break;
+            case PDOP_PUSH_I:
+                if (!cplx_pass) return -2;
+                FN(jconst)(st[d], I); ++d; break;
+            case PDOP_ADD: for (int i = 0; i < NC(K); ++i) u[i] = u[i] + t[i]; --d; break;
+            case PDOP_SUB: for (int i = 0; i < NC(K); ++i) u[i] = u[i] - t[i]; --d; break;
+            case PDOP_RSUB: for (int i = 0; i < NC(K); ++i) u[i] = t[i] - u[i]; --d; break;
+            case PDOP_MUL: FN(jmul)(u, t, u, K); --d; break;
+            case PDOP_DIV: FN(jdiv)(u, t, u, K); --d; break;
+            case PDOP_RDIV: FN(jdiv)(t, u, u, K); --d; break;
+            case PDOP_ADDC: t[0] += imm; break;
+            case PDOP_MULC: for (int i = 0; i < NC(K); ++i) t[i] *= imm; break;
+            case PDOP_RDIVC: { S c[NCMAX]; FN(jconst)(c, imm); FN(jdiv)(c, t, t, K); break; }
+            case PDOP_NEG: for (int i = 0; i < NC(K); ++i) t[i] = -t[i]; break;
+            case PDOP_ADD_X: t[0] += px; t[IDX(1, 0)] += 1; break;
+            case PDOP_ADD_Y: t[0] += py; t[IDX(0, 1)] += 1; break;
+            case PDOP_SUB_X: t[0] -= px; t[IDX(1, 0)] -= 1; break;
+            case PDOP_SUB_Y: t[0] -= py; t[IDX(0, 1)] -= 1; break;
+            case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: {
+                S v[NCMAX];
+                int isx = (op == PDOP_MUL_X || op == PDOP_DIV_X);
+                FN(jconst)(v, isx ? px : py);
+                v[isx ? IDX(1, 0) : IDX(0, 1)] = 1;
+                if (op == PDOP_MUL_X || op == PDOP_MUL_Y) FN(jmul)(t, v, t, K);
+                else FN(jdiv)(t, v, t, K);
+                break;
+            }
+            case PDOP_POWN: {
+                int n = (int)((word >> 8) & 0xffu);
+                S b[NCMAX];
+                memcpy(b, t, sizeof(S) * NC(K));
+                for (int k = 1; k < n; ++k) FN(jmul)(t, b, t, K);
+                break;
+            }
+            case PDOP_POW: case PDOP_SQRT: {
+                double a = (op == PDOP_SQRT) ? 0.5 : imm;
+                S x0 = t[0];
+                f[0] = FN(spow)(x0, a, cplx_pass);
+                for (int k = 1; k <= K; ++k) f[k] = f[k - 1] * ((a - (k - 1)) / k) / x0;
+                FN(jcompose)(t, f, K);
+                break;
+            }
+            case PDOP_EXP: {
+                S e = cplx_pass ? cexp(t[0]) : exp(creal(t[0]));
+                double fact = 1;
+                for (int k = 0; k <= K; ++k) { if (k) fact *= k; f[k] = e / fact; }
+                FN(jcompose)(t, f, K);
+                break;
+            }
+            case PDOP_LOG: {
+                S x0 = t[0];
+                f[0] = cplx_pass ? clog(x0) : (creal(x0) > 0 ? log(creal(x0)) : (creal(x0) == 0 ? -INFINITY : NAN));
+                for (int k = 1; k <= K; ++k) f[k] = ((k & 1) ? 1.0 : -1.0) / (k * FN(spow)(x0, k, cplx_pass));
+                FN(jcompose)(t, f, K);
+                break;
+            }
+            case PDOP_ABS: {
+                double sg;
+                if (cimag(t[0]) != 0) sg = NAN;
+                else sg = creal(t[0]) > 0 ? 1 : (creal(t[0]) < 0 ? -1 : NAN);
+                for (int i = 0; i < NC(K); ++i) t[i] *= sg;
+                break;
+            }
+            case PDOP_UNSUPPORTED: return -3;
+            default: return -3;
+        }
+        if (d > 15 || d < 1) return -4;
+    }
+    if (d != 1) return -5;
+    memcpy(out, st[0], sizeof(S) * NC(K));
+    return 0;
+}
+
+/* partial derivative u_{ij} = i! j! c_ij */
+static S FN(partial)(const S* c, int i, int j) {
+    static const double fct[5] = {1, 1, 2, 6, 24};
+    return c[IDX(i, j)] * (fct[i] * fct[j]);
+}
+
+/* Force-free determinant in closed form from partials (validator.py:323-347, Omega = 0).
+ * mag != 0: every term replaced by its magnitude (the scale S). */
+static S FN(ff_det)(const S* c, double rho, int mag) {
+#define M_(x) (mag ? (S)cabs(x) : (x))
+#define SUB_(a, b) (mag ? ((a) + (b)) : ((a) - (b)))
+    S u10 = M_(FN(partial)(c, 1, 0)), u01 = M_(FN(partial)(c, 0, 1));
+    S u20 = M_(FN(partial)(c, 2, 0)), u11 = M_(FN(partial)(c, 1, 1)), u02 = M_(FN(partial)(c, 0, 2));
+    S u30 = M_(FN(partial)(c, 3, 0)), u21 = M_(FN(partial)(c, 2, 1)), u12 = M_(FN(partial)(c, 1, 2));
+    S u03 = M_(FN(partial)(c, 0, 3));
+    S u40 = M_(FN(partial)(c, 4, 0)), u31 = M_(FN(partial)(c, 3, 1)), u22 = M_(FN(partial)(c, 2, 2));
+    S u13 = M_(FN(partial)(c, 1, 3)), u04 = M_(FN(partial)(c, 0, 4));
+    double r1 = 1.0 / rho, r2 = r1 * r1, r3 = r2 * r1;
+    S p = u10, q = u01;
+    /* A = u20 + u02 - u10/rho and its partials */
+    S Ar = u30 + u12 + SUB_(0, u20 * r1) + u10 * r2;
+    S Az = u21 + SUB_(u03, u11 * r1);
+    S Arr = u40 + u22 + SUB_(0, u30 * r1) + 2 * u20 * r2 + SUB_(0, 2 * u10 * r3);
+    S Arz = u31 + u13 + SUB_(0, u21 * r1) + u11 * r2;
+    S Azz = u22 + SUB_(u04, u12 * r1);
+    /* B = p^2 + q^2 */
+    S Br = 2 * (p * u20 + q * u11);
+    S Bz = 2 * (p * u11 + q * u02);
+    S Brr = 2 * (u20 * u20 + p * u30 + u11 * u11 + q * u21);
+    S Brz = 2 * (u11 * u20 + p * u21 + u02 * u11 + q * u12);
+    S Bzz = 2 * (u11 * u11 + p * u12 + u02 * u02 + q * u03);
+    /* L_T f = q f_r - p f_z;  L_T^2 f = q (L_T f)_r - p (L_T f)_z */
+    S LA = SUB_(q * Ar, p * Az), LB = SUB_(q * Br, p * Bz);
+    S LAr = SUB_(u11 * Ar + q * Arr, u20 * Az + p * Arz);
+    S LAz = SUB_(u02 * Ar + q * Arz, u11 * Az + p * Azz);
+    S LBr = SUB_(u11 * Br + q * Brr, u20 * Bz + p * Brz);
+    S LBz = SUB_(u02 * Br + q * Brz, u11 * Bz + p * Bzz);
+    S L2A = SUB_(q * LAr, p * LAz), L2B = SUB_(q * LBr, p * LBz);
+    return SUB_(LA * L2B, LB * L2A);
+#undef M_
+#undef SUB_
+}

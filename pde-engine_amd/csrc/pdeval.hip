@@ -1,0 +1,442 @@
+// pdeval.hip -- libpdeval.so: the C ABI (include/pdeval.h) around the gfx950 kernels.
+//
+// Host side of the boundary: contexts (one per GPU), the sample-point tables of each problem
+// (reference points first, then the nx*ny grid), device work lists for the two follow-up
+// passes (deep-stack programs, complex-valued candidates) and the launch sequence.  All device
+// allocation happens at create time or when a batch outgrows the scratch lists, never inside
+// an already-sized hot call, so pdeval_validate_device can be captured in a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pdeval.h"
+#include "pdeval_kernels.h"
+
+using namespace pd;
+
+#define PD_VERSION "pdeval 0.1 gfx950"
+
+struct pdeval_ctx {
+    int device = 0;
+    int problem = 0;
+    int n_ref = 0, n_pts = 0;
+    int fp_pts[PDEVAL_FP_N] = {0, 0, 0, 0};
+    hipStream_t stream = nullptr;
+    double* d_px = nullptr;
+    double* d_py = nullptr;
+    double* d_kc = nullptr;
+    // scratch: work lists and their counters
+    int64_t cap = 0;
+    int64_t* d_defer = nullptr;
+    int64_t* d_cplx = nullptr;
+    int32_t* d_counts = nullptr;  // [0] defer, [1] cplx
+    // host-path staging
+    int64_t hcap_words = 0, hcap_n = 0;
+    int32_t* d_ops = nullptr;
+    int64_t* d_off = nullptr;
+    uint8_t* d_outbuf = nullptr;
+    int64_t outbuf_bytes = 0;
+    std::string err;
+};
+
+static thread_local std::string g_err;
+
+#define HIPCHK(ctx, expr)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+            return PDEVAL_ERR_HIP;                                                          \
+        }                                                                                   \
+    } while (0)
+
+// ---------------------------------------------------------------------------- point tables
+namespace {
+
+struct Grid {
+    double x_lo, x_hi, nx, y_lo, y_hi, ny, x_ph, y_ph;
+};
+
+// DESIGN.md "Grids": cell-offset grids that avoid the coordinate singular sets exactly.
+Grid default_grid(int problem) {
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE)
+        return {0.05, 3.0, 64, -2.0, 2.0, 64, 0.37, 0.41};
+    const double r_plus = 1.0 + std::sqrt(0.99);  // M + sqrt(M^2 - a^2), M = 1, a = 1/10
+    return {r_plus + 0.1, r_plus + 6.1, 64, -0.98, 0.98, 64, 0.37, 0.41};
+}
+
+// Kerr operator coefficients (kerr validator.py:69-91, M = 1, a = 1/10):
+// L[u] = G/(1-x^2) u_rr + G/Delta u_xx + d_r(G)/(1-x^2) u_r + d_x(G)/Delta u_x
+void kerr_coeffs(double r_, double x_, double* k) {
+    const long double M = 1.0L, a = 0.1L, r = r_, x = x_;
+    const long double s = r * r + a * a * x * x;
+    const long double G = 1.0L - 2.0L * M * r / s;
+    const long double Gr = 2.0L * M * (r * r - a * a * x * x) / (s * s);
+    const long double Gx = 4.0L * M * a * a * r * x / (s * s);
+    const long double D = r * r - 2.0L * M * r + a * a;
+    const long double w = 1.0L - x * x;
+    k[0] = (double)(G / w);
+    k[1] = (double)(G / D);
+    k[2] = (double)(Gr / w);
+    k[3] = (double)(Gx / D);
+}
+
+}  // namespace
+
+extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, int n_grid,
+                             pdeval_ctx** out) {
+    if (!out || (problem_id != PDEVAL_PROBLEM_FORCE_FREE && problem_id != PDEVAL_PROBLEM_KERR)) {
+        g_err = "pdeval_create: bad argument";
+        return PDEVAL_ERR_ARG;
+    }
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        g_err = "pdeval_create: no HIP device";
+        return PDEVAL_ERR_NODEVICE;
+    }
+    if (device_id < 0 || device_id >= ndev) {
+        g_err = "pdeval_create: device id out of range";
+        return PDEVAL_ERR_ARG;
+    }
+    pdeval_ctx* c = new pdeval_ctx();
+    c->device = device_id;
+    c->problem = problem_id;
+    Grid g = default_grid(problem_id);
+    if (grid && n_grid >= 8) std::memcpy(&g, grid, sizeof(Grid));
+    const int nx = (int)g.nx, ny = (int)g.ny;
+    if (nx <= 0 || ny <= 0 || nx * ny > (1 << 22)) {
+        delete c;
+        g_err = "pdeval_create: bad grid";
+        return PDEVAL_ERR_ARG;
+    }
+    std::vector<double> px, py;
+    if (problem_id == PDEVAL_PROBLEM_FORCE_FREE) {
+        // the paper's test point (rho, z) = (4/5, 6/7), validator.py:296-297
+        px = {0.8};
+        py = {6.0 / 7.0};
+    } else {
+        // kerr validator.py:167-171
+        px = {2.5, 7.0 / 3.0, 5.0};
+        py = {0.6, 1.0 / 3.0, -0.4};
+    }
+    c->n_ref = (int)px.size();
+    for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < ny; ++j) {
+            px.push_back(g.x_lo + (i + g.x_ph) * ((g.x_hi - g.x_lo) / nx));
+            py.push_back(g.y_lo + (j + g.y_ph) * ((g.y_hi - g.y_lo) / ny));
+        }
+    c->n_pts = (int)px.size();
+    const int G = nx * ny;
+    c->fp_pts[0] = 0;
+    for (int f = 1; f < PDEVAL_FP_N; ++f) c->fp_pts[f] = c->n_ref + (int)((int64_t)G * f / PDEVAL_FP_N) + 7 % G;
+    std::vector<double> kc;
+    if (problem_id == PDEVAL_PROBLEM_KERR) {
+        kc.resize(4 * px.size());
+        for (size_t p = 0; p < px.size(); ++p) kerr_coeffs(px[p], py[p], &kc[4 * p]);
+    }
+    auto fail = [&](const char* what, hipError_t e) {
+        g_err = std::string(what) + ": " + hipGetErrorString(e);
+        pdeval_destroy(c);
+        return PDEVAL_ERR_HIP;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device_id)) != hipSuccess) return fail("hipSetDevice", e);
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
+        return fail("hipStreamCreate", e);
+    const size_t pb = px.size() * sizeof(double);
+    if ((e = hipMalloc(&c->d_px, pb)) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc(&c->d_py, pb)) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMemcpy(c->d_px, px.data(), pb, hipMemcpyHostToDevice)) != hipSuccess) return fail("hipMemcpy", e);
+    if ((e = hipMemcpy(c->d_py, py.data(), pb, hipMemcpyHostToDevice)) != hipSuccess) return fail("hipMemcpy", e);
+    if (!kc.empty()) {
+        if ((e = hipMalloc(&c->d_kc, kc.size() * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
+        if ((e = hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+            return fail("hipMemcpy", e);
+    }
+    if ((e = hipMalloc(&c->d_counts, 4 * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
+    *out = c;
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_destroy(pdeval_ctx* c) {
+    if (!c) return PDEVAL_ERR_ARG;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (void* p : {(void*)c->d_px, (void*)c->d_py, (void*)c->d_kc, (void*)c->d_defer, (void*)c->d_cplx,
+                    (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
+        if (p) hipFree(p);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return PDEVAL_OK;
+}
+
+extern "C" const char* pdeval_last_error(pdeval_ctx* c) { return c ? c->err.c_str() : g_err.c_str(); }
+extern "C" int pdeval_n_ref_points(pdeval_ctx* c) { return c ? c->n_ref : -1; }
+extern "C" int pdeval_n_points(pdeval_ctx* c) { return c ? c->n_pts : -1; }
+extern "C" const char* pdeval_version(void) { return PD_VERSION; }
+
+extern "C" int pdeval_default_params(int problem_id, pdeval_params* p) {
+    if (!p) return PDEVAL_ERR_ARG;
+    // DESIGN.md "Zero test": thresholds calibrated on the reference fixtures
+    p->tau_point = 1e-10;
+    p->tau_grid = 1e-7;
+    p->kerr_abs_tol = 1e-10;  // kerr validator.py:190
+    p->full_grid = 1;
+    p->max_bad = 0;
+    (void)problem_id;
+    return PDEVAL_OK;
+}
+
+// ---------------------------------------------------------------------------- program checks
+static int op_has_imm(uint32_t op) {
+    return op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC || op == PDOP_POW;
+}
+static int op_stack_delta(uint32_t op, int* need) {
+    switch (op) {
+        case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I: case PDOP_UNSUPPORTED:
+            *need = 0; return 1;
+        case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: case PDOP_MUL: case PDOP_DIV: case PDOP_RDIV:
+            *need = 2; return -1;
+        default:
+            if (op > 0 && op < PDOP_COUNT_) { *need = 1; return 0; }
+            *need = -1; return 0;
+    }
+}
+
+// Returns the max stack depth of a program (header word included), or < 0 if malformed.
+extern "C" int pdeval_program_depth(const int32_t* ops, int64_t n_words) {
+    if (!ops || n_words < 2) return -1;
+    if ((ops[0] & 0xff) != 0) return -2;
+    int d = 0, dmax = 0;
+    for (int64_t pc = 1; pc < n_words;) {
+        const uint32_t op = (uint32_t)ops[pc] & 0xffu;
+        int need;
+        const int dd = op_stack_delta(op, &need);
+        if (need < 0) return -3;
+        if (d < need) return -4;
+        if (op == PDOP_POWN) {
+            const int n = (ops[pc] >> 8) & 0xff;
+            if (n < 2 || n > 16) return -5;
+        }
+        d += dd;
+        if (d > dmax) dmax = d;
+        pc += 1 + (op_has_imm(op) ? 2 : 0);
+        if (pc > n_words) return -6;
+    }
+    if (d != 1) return -7;
+    if (dmax != ((ops[0] >> 8) & 0xff)) return -8;  // header must state the true depth
+    return dmax;
+}
+
+// Algorithmic FP64 flop model per sample point (DESIGN.md "Roofline"): jet work of each
+// opcode at the problem's order plus the residual epilogue.
+extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words) {
+    const bool ff = problem_id == PDEVAL_PROBLEM_FORCE_FREE;
+    const int K = ff ? 4 : 2;
+    const double NC = (K + 1) * (K + 2) / 2.0;
+    // full product: 2 * C(K+3, 3) - NC flops (K=4: 140-15 = 125; K=2: 40-6 = 34)
+    const double mulf = ff ? 125.0 : 34.0;
+    const double divf = mulf + NC + 10.0;
+    // Horner composition: sum over levels (2*#products) + coefficient chain
+    const double compf = ff ? (2.0 * 91.0 + 3.0 * K) : (2.0 * 11.0 + 3.0 * K);
+    double f = 0.0;
+    for (int64_t pc = 1; pc < n_words;) {
+        const uint32_t op = (uint32_t)ops[pc] & 0xffu;
+        switch (op) {
+            case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: f += NC; break;
+            case PDOP_MUL: f += mulf; break;
+            case PDOP_DIV: case PDOP_RDIV: case PDOP_RDIVC: f += divf; break;
+            case PDOP_ADDC: case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: f += 2; break;
+            case PDOP_MULC: case PDOP_NEG: case PDOP_ABS: f += NC; break;
+            case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: f += 2 * NC; break;
+            case PDOP_POWN: {
+                int n = (ops[pc] >> 8) & 0xff, m = 0;
+                while (n > 1) { m += 1 + (n & 1); n >>= 1; }
+                f += m * mulf;
+                break;
+            }
+            case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: f += compf; break;
+            default: break;
+        }
+        pc += 1 + (op_has_imm(op) ? 2 : 0);
+    }
+    // epilogue: force-free determinant + its magnitude shadow; Kerr 4-term operator + scale
+    f += ff ? 2.0 * 160.0 : 16.0;
+    return f;
+}
+
+// ---------------------------------------------------------------------------- launches
+static int ensure_scratch(pdeval_ctx* c, int64_t n) {
+    if (n <= c->cap) return PDEVAL_OK;
+    if (c->d_defer) hipFree(c->d_defer);
+    if (c->d_cplx) hipFree(c->d_cplx);
+    c->d_defer = c->d_cplx = nullptr;
+    c->cap = 0;
+    const int64_t cap = n < 1024 ? 1024 : n;
+    HIPCHK(c, hipMalloc(&c->d_defer, cap * sizeof(int64_t)));
+    HIPCHK(c, hipMalloc(&c->d_cplx, cap * sizeof(int64_t)));
+    c->cap = cap;
+    return PDEVAL_OK;
+}
+
+template <int PROB>
+static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, const int64_t* d_off, int64_t n,
+                      const pdeval_params& prm, const pdeval_outputs& o, hipStream_t s) {
+    KernelArgs a{};
+    a.ops = d_ops;
+    a.offsets = d_off;
+    a.n_words = n_words;
+    a.n = n;
+    a.px = c->d_px;
+    a.py = c->d_py;
+    a.kc = c->d_kc;
+    a.n_ref = c->n_ref;
+    a.n_pts = c->n_pts;
+    for (int f = 0; f < PDEVAL_FP_N; ++f) a.fp_pts[f] = c->fp_pts[f];
+    a.prm = prm;
+    a.out = o;
+    a.defer_list = c->d_defer;
+    a.defer_count = c->d_counts;
+    a.cplx_list = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? c->d_cplx : nullptr;
+    a.cplx_count = c->d_counts + 1;
+    a.list_capacity = c->cap;
+    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, 4 * sizeof(int32_t), s));
+    constexpr int WPB = 4;  // waves (candidates) per 256-thread block
+    const int64_t blocks = (n + WPB - 1) / WPB;
+    // pass 1: programs whose stack fits 2 jets (>92 % of force-free depth 4), one wave per
+    // candidate; deeper programs are appended to a device list
+    a.defer_list = c->d_defer;
+    a.defer_count = c->d_counts + 0;
+    hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    HIPCHK(c, hipGetLastError());
+    // pass 2: the deferred programs, persistent over the device list (stack <= 8)
+    KernelArgs b = a;
+    b.list = c->d_defer;
+    b.list_count = c->d_counts + 0;
+    b.defer_list = nullptr;  // depth <= PDEVAL_MAX_STACK is guaranteed by the flattener
+    const int64_t pblocks = std::min<int64_t>(blocks, 1024);
+    hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>), dim3((unsigned)pblocks),
+                       dim3(256), 0, s, b);
+    HIPCHK(c, hipGetLastError());
+    if (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+        // pass 3: candidates not real at the reference point, in complex arithmetic
+        KernelArgs x = a;
+        x.list = c->d_cplx;
+        x.list_count = c->d_counts + 1;
+        x.cplx_list = nullptr;
+        x.defer_list = nullptr;
+        const int64_t cblocks = std::min<int64_t>(blocks, 256);
+        hipLaunchKernelGGL((validate_kernel<PROB, cplx, 4, true>), dim3((unsigned)cblocks),
+                           dim3(256), 0, s, x);
+        HIPCHK(c, hipGetLastError());
+    }
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words,
+                                      const int64_t* d_offsets, int64_t n, const pdeval_params* params,
+                                      const pdeval_outputs* d_out, void* stream, int zero_bits) {
+    if (!c || !d_out || n < 0 || (n > 0 && (!d_ops || !d_offsets)) || n_words < 0) {
+        if (c) c->err = "pdeval_validate_device: bad argument";
+        return PDEVAL_ERR_ARG;
+    }
+    if (n == 0) return PDEVAL_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    pdeval_params prm;
+    if (params) prm = *params;
+    else pdeval_default_params(c->problem, &prm);
+    int rc = ensure_scratch(c, n);
+    if (rc) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (zero_bits && d_out->verdict_bits)
+        HIPCHK(c, hipMemsetAsync(d_out->verdict_bits, 0, ((n + 31) / 32) * 4, s));
+    if (c->problem == PDEVAL_PROBLEM_FORCE_FREE)
+        return launch_all<PDEVAL_PROBLEM_FORCE_FREE>(c, d_ops, n_words, d_offsets, n, prm, *d_out, s);
+    return launch_all<PDEVAL_PROBLEM_KERR>(c, d_ops, n_words, d_offsets, n, prm, *d_out, s);
+}
+
+extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t n_words,
+                                     const int64_t* offsets, int64_t n, const pdeval_params* params,
+                                     pdeval_outputs* out) {
+    if (!c || !out || n < 0 || (n > 0 && (!ops || !offsets))) {
+        if (c) c->err = "pdeval_validate_batch: bad argument";
+        return PDEVAL_ERR_ARG;
+    }
+    if (n == 0) return PDEVAL_OK;
+    if (offsets[0] != 0 || offsets[n] != n_words) {
+        c->err = "pdeval_validate_batch: offsets must start at 0 and end at n_words";
+        return PDEVAL_ERR_ARG;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        if (offsets[i + 1] < offsets[i]) {
+            c->err = "pdeval_validate_batch: offsets not monotone at " + std::to_string(i);
+            return PDEVAL_ERR_ARG;
+        }
+        const int d = pdeval_program_depth(ops + offsets[i], offsets[i + 1] - offsets[i]);
+        if (d < 0 || d > PDEVAL_MAX_STACK) {
+            c->err = "pdeval_validate_batch: malformed program " + std::to_string(i) + " (code " +
+                     std::to_string(d) + ")";
+            return PDEVAL_ERR_PROGRAM;
+        }
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    if (n_words > c->hcap_words) {
+        if (c->d_ops) hipFree(c->d_ops);
+        c->d_ops = nullptr;
+        c->hcap_words = 0;
+        HIPCHK(c, hipMalloc(&c->d_ops, n_words * sizeof(int32_t)));
+        c->hcap_words = n_words;
+    }
+    if (n + 1 > c->hcap_n) {
+        if (c->d_off) hipFree(c->d_off);
+        c->d_off = nullptr;
+        c->hcap_n = 0;
+        HIPCHK(c, hipMalloc(&c->d_off, (n + 1) * sizeof(int64_t)));
+        c->hcap_n = n + 1;
+    }
+    // device output block
+    const int64_t nb = ((n + 31) / 32) * 4;
+    const int64_t sz_bits = (nb + 15) / 16 * 16, sz_st = (n + 15) / 16 * 16;
+    const int64_t need = sz_bits + sz_st + 8 * n * (3 + c->n_ref + PDEVAL_FP_N) + 8 * n * 2;
+    if (need > c->outbuf_bytes) {
+        if (c->d_outbuf) hipFree(c->d_outbuf);
+        c->d_outbuf = nullptr;
+        c->outbuf_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_outbuf, need));
+        c->outbuf_bytes = need;
+    }
+    uint8_t* p = c->d_outbuf;
+    pdeval_outputs d{};
+    d.verdict_bits = p; p += sz_bits;
+    d.status = p; p += sz_st;
+    d.q_ref = (double*)p; p += 8 * n;
+    d.q_grid = (double*)p; p += 8 * n;
+    d.res_ref = (double*)p; p += 8 * n * c->n_ref;
+    d.fingerprint = (double*)p; p += 8 * n * PDEVAL_FP_N;
+    d.n_bad = (int32_t*)p; p += 4 * n;
+    d.n_nonfinite = (int32_t*)p; p += 4 * n;
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(c->d_ops, ops, n_words * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_off, offsets, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    int rc = pdeval_validate_device(c, c->d_ops, n_words, c->d_off, n, params, &d, s, 1);
+    if (rc) return rc;
+    auto dl = [&](void* h, const void* dv, size_t bytes) -> int {
+        if (h) HIPCHK(c, hipMemcpyAsync(h, dv, bytes, hipMemcpyDeviceToHost, s));
+        return PDEVAL_OK;
+    };
+    if ((rc = dl(out->verdict_bits, d.verdict_bits, (n + 7) / 8))) return rc;
+    if ((rc = dl(out->status, d.status, n))) return rc;
+    if ((rc = dl(out->q_ref, d.q_ref, 8 * n))) return rc;
+    if ((rc = dl(out->q_grid, d.q_grid, 8 * n))) return rc;
+    if ((rc = dl(out->res_ref, d.res_ref, 8 * n * c->n_ref))) return rc;
+    if ((rc = dl(out->fingerprint, d.fingerprint, 8 * n * PDEVAL_FP_N))) return rc;
+    if ((rc = dl(out->n_bad, d.n_bad, 4 * n))) return rc;
+    if ((rc = dl(out->n_nonfinite, d.n_nonfinite, 4 * n))) return rc;
+    HIPCHK(c, hipStreamSynchronize(s));
+    return PDEVAL_OK;
+}

@@ -1,0 +1,168 @@
+"""ctypes binding of libpdeval.so (the C ABI declared in ``include/pdeval.h``).
+
+This is the Python side of the drop-in boundary: the reference's validator plugins are
+Python objects called once per candidate (``problems/__init__.py:52``); here one call
+validates a whole batch through the C ABI.  There is deliberately no fallback: if the
+library is missing or no GPU is present, :func:`load` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from .opcodes import FP_N
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('PDEVAL_LIB', os.path.join(_HERE, '..', 'lib', 'libpdeval.so'))
+
+EXPORTS = (
+    'pdeval_create', 'pdeval_destroy', 'pdeval_last_error', 'pdeval_n_ref_points',
+    'pdeval_n_points', 'pdeval_default_params', 'pdeval_validate_batch',
+    'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
+)
+
+
+class Params(C.Structure):
+    _fields_ = [('tau_point', C.c_double), ('tau_grid', C.c_double),
+                ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32)]
+
+
+class Outputs(C.Structure):
+    _fields_ = [('verdict_bits', C.c_void_p), ('status', C.c_void_p), ('q_ref', C.c_void_p),
+                ('res_ref', C.c_void_p), ('q_grid', C.c_void_p), ('n_bad', C.c_void_p),
+                ('n_nonfinite', C.c_void_p), ('fingerprint', C.c_void_p)]
+
+
+class PdevalError(RuntimeError):
+    pass
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def load(path: Optional[str] = None) -> C.CDLL:
+    """Load libpdeval.so and declare its signatures (raises if it is missing)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = os.path.abspath(path or LIB_PATH)
+    if not os.path.exists(p):
+        raise PdevalError(f'libpdeval.so not found at {p}: run __graft_entry__.build()')
+    lib = C.CDLL(p)
+    vp, i32, i64, dbl = C.c_void_p, C.c_int32, C.c_int64, C.c_double
+    lib.pdeval_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double), C.c_int, C.POINTER(vp)]
+    lib.pdeval_destroy.argtypes = [vp]
+    lib.pdeval_last_error.argtypes = [vp]
+    lib.pdeval_last_error.restype = C.c_char_p
+    lib.pdeval_n_ref_points.argtypes = [vp]
+    lib.pdeval_n_points.argtypes = [vp]
+    lib.pdeval_default_params.argtypes = [C.c_int, C.POINTER(Params)]
+    lib.pdeval_validate_batch.argtypes = [vp, vp, i64, vp, i64, C.POINTER(Params), C.POINTER(Outputs)]
+    lib.pdeval_validate_device.argtypes = [vp, vp, i64, vp, i64, C.POINTER(Params),
+                                           C.POINTER(Outputs), vp, C.c_int]
+    lib.pdeval_program_depth.argtypes = [vp, i64]
+    lib.pdeval_program_flops.argtypes = [C.c_int, vp, i64]
+    lib.pdeval_program_flops.restype = dbl
+    lib.pdeval_version.restype = C.c_char_p
+    for name in EXPORTS:
+        getattr(lib, name)   # every symbol of the header must resolve
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def default_params(problem_id: int) -> Params:
+    p = Params()
+    _check(None, load().pdeval_default_params(problem_id, C.byref(p)))
+    return p
+
+
+def _check(ctx, rc: int):
+    if rc != 0:
+        msg = load().pdeval_last_error(ctx)
+        raise PdevalError(f'pdeval error {rc}: {msg.decode() if msg else ""}')
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+class Context:
+    """One libpdeval context = one GPU + one problem's sample grid."""
+
+    def __init__(self, problem_id: int, device: int = 0, grid: Optional[np.ndarray] = None):
+        lib = load()
+        h = C.c_void_p()
+        gp = None
+        ng = 0
+        if grid is not None:
+            g = np.ascontiguousarray(grid, dtype=np.float64)
+            gp, ng = g.ctypes.data_as(C.POINTER(C.c_double)), g.size
+        rc = lib.pdeval_create(device, problem_id, gp, ng, C.byref(h))
+        if rc != 0:
+            raise PdevalError(f'pdeval_create failed ({rc}): {lib.pdeval_last_error(None).decode()}')
+        self.h = h
+        self.lib = lib
+        self.problem_id = problem_id
+        self.device = device
+        self.n_ref = lib.pdeval_n_ref_points(h)
+        self.n_points = lib.pdeval_n_points(h)
+
+    def close(self):
+        if self.h:
+            self.lib.pdeval_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def validate(self, ops: np.ndarray, offsets: np.ndarray, params: Optional[Params] = None):
+        """Host arrays in, dict of per-candidate numpy outputs back (synchronous)."""
+        ops = np.ascontiguousarray(ops, dtype=np.int32)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        n = len(offsets) - 1
+        res = {
+            'verdict_bits': np.zeros((n + 7) // 8, dtype=np.uint8),
+            'status': np.zeros(n, dtype=np.uint8),
+            'q_ref': np.zeros(n, dtype=np.float64),
+            'res_ref': np.zeros(n * self.n_ref, dtype=np.float64),
+            'q_grid': np.zeros(n, dtype=np.float64),
+            'n_bad': np.zeros(n, dtype=np.int32),
+            'n_nonfinite': np.zeros(n, dtype=np.int32),
+            'fingerprint': np.zeros(n * FP_N, dtype=np.float64),
+        }
+        out = Outputs(*[_ptr(res[f]) for f, _ in Outputs._fields_])
+        prm = params if params is not None else default_params(self.problem_id)
+        rc = self.lib.pdeval_validate_batch(self.h, _ptr(ops), ops.size, _ptr(offsets), n,
+                                            C.byref(prm), C.byref(out))
+        _check(self.h, rc)
+        res['res_ref'] = res['res_ref'].reshape(n, self.n_ref)
+        res['fingerprint'] = res['fingerprint'].reshape(n, FP_N)
+        res['verdict'] = np.unpackbits(res['verdict_bits'], bitorder='little')[:n].astype(bool)
+        return res
+
+    def validate_device(self, d_ops: int, n_words: int, d_offsets: int, n: int, d_out: Outputs,
+                        params: Optional[Params] = None, stream: int = 0, zero_bits: bool = True):
+        """Device pointers in and out (inputs resident in HBM), asynchronous on `stream`."""
+        prm = params if params is not None else default_params(self.problem_id)
+        if not stream:
+            raise PdevalError('validate_device needs an explicit (non-null) HIP stream handle')
+        rc = self.lib.pdeval_validate_device(self.h, d_ops, n_words, d_offsets, n, C.byref(prm),
+                                             C.byref(d_out), stream, int(zero_bits))
+        _check(self.h, rc)
+
+
+def program_depth(words: np.ndarray) -> int:
+    w = np.ascontiguousarray(words, dtype=np.int32)
+    return load().pdeval_program_depth(_ptr(w), w.size)
+
+
+def program_flops(problem_id: int, words: np.ndarray) -> float:
+    w = np.ascontiguousarray(words, dtype=np.int32)
+    return load().pdeval_program_flops(problem_id, _ptr(w), w.size)

@@ -1,0 +1,380 @@
+"""Host flattener: SymPy expression tree -> postfix jet program (``include/pdeval.h`` format).
+
+This is the host half of the hot path.  The reference parses each
+normalized candidate string with ``sp.sympify(s, locals=symbols + constants + UNARY_OPS)``
+(``general_method_paper_reproduction.py:1257, :1767``) and hands the tree to ``validate``.
+We take the same tree and compile it for the kernel:
+
+* n-ary ``Add``/``Mul`` are binarized; terms with a negative numeric coefficient become
+  subtractions, factors ``b**-n`` (integer n) move to a single denominator (one jet division
+  instead of a reciprocal composition);
+* operands that are leaves (a coordinate or a constant) fuse into the consuming opcode
+  (``MUL_X``, ``ADDC`` ...), so they never occupy a stack slot;
+* children are emitted in Sethi-Ullman order (the operand needing more stack goes first, with
+  reversed opcodes ``RSUB``/``RDIV`` for non-commutative ops) which keeps the operand stack --
+  held in VGPRs on the device -- as shallow as the tree allows;
+* constants are folded to IEEE doubles (rationals correctly rounded from the exact p/q).
+
+The output is a list of int32 words: a header (opcode 0, stack depth in bits 8-15, flags in
+bits 16-31), then the postfix body; opcodes with an immediate are followed by its two words.
+"""
+from __future__ import annotations
+
+import math
+import struct
+from fractions import Fraction
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import sympy as sp
+
+from .opcodes import PDOP, HAS_IMM, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD
+
+
+class Unsupported(Exception):
+    """The tree uses a construct the kernels do not evaluate."""
+
+
+# --------------------------------------------------------------------------- IR
+# nodes: ('x',) ('y',) ('i',) ('c', float)
+#        (op, child) for op in neg sqrt exp log abs;  ('pown', child, n);  ('pow', child, alpha)
+#        (op, a, b) for op in add sub mul div
+def _is_leaf(n) -> bool:
+    return n[0] in ('x', 'y', 'c')
+
+
+def _const(v) -> tuple:
+    return ('c', float(v))
+
+
+def _num_to_float(e: sp.Basic) -> float:
+    if e.is_Integer:
+        return float(int(e))
+    if e.is_Rational:
+        # int / int true division in Python is correctly rounded
+        return int(e.p) / int(e.q)
+    return float(e)
+
+
+class _Lower:
+    def __init__(self, x_sym: sp.Symbol, y_sym: sp.Symbol, consts: Dict[sp.Symbol, sp.Basic]):
+        self.x = x_sym
+        self.y = y_sym
+        self.consts = consts
+        self.uses_i = False
+
+    def node(self, e: sp.Basic):
+        if e.is_Symbol:
+            if e == self.x or e.name == self.x.name:
+                return ('x',)
+            if e == self.y or e.name == self.y.name:
+                return ('y',)
+            for s, v in self.consts.items():
+                if e == s or e.name == s.name:
+                    return _const(_num_to_float(sp.nsimplify(v)) if not isinstance(v, float) else v)
+            raise Unsupported(f'free symbol {e}')
+        if e is sp.nan or e is sp.zoo or e is sp.oo or e is sp.S.NegativeInfinity:
+            return _const(float('nan'))     # the driver's pre-validate filter drops these
+        if e.is_Number:
+            return _const(_num_to_float(e))
+        if e is sp.E:
+            return _const(math.e)
+        if e is sp.pi:
+            return _const(math.pi)
+        if e is sp.I:
+            self.uses_i = True
+            return ('i',)
+        if e.is_Add:
+            return self.add(e)
+        if e.is_Mul:
+            return self.mul(e)
+        if e.is_Pow:
+            return self.pow(e.base, e.exp)
+        if isinstance(e, sp.exp):
+            return ('exp', self.node(e.args[0]))
+        if isinstance(e, sp.log) and len(e.args) == 1:
+            return ('log', self.node(e.args[0]))
+        if isinstance(e, sp.Abs):
+            return ('abs', self.node(e.args[0]))
+        raise Unsupported(f'{type(e).__name__}')
+
+    def add(self, e: sp.Add):
+        const = 0.0
+        have_const = False
+        terms: List[Tuple[int, tuple]] = []
+        for t in e.args:
+            if t.is_Number and t.is_real:
+                const += _num_to_float(t)
+                have_const = True
+                continue
+            sign = 1
+            if t.is_Mul and t.args[0].is_Number and t.args[0].is_real and t.args[0] < 0:
+                t = sp.Mul(-t.args[0], *t.args[1:], evaluate=False) if t.args[0] != -1 \
+                    else sp.Mul(*t.args[1:], evaluate=False)
+                sign = -1
+            terms.append((sign, self.node(t)))
+        if not terms:
+            return _const(const)
+        # positive terms first (so no leading negation is needed), heavy operands first
+        terms.sort(key=lambda st: (st[0] < 0, -_need(st[1])))
+        sign, acc = terms[0]
+        if sign < 0:
+            acc = ('neg', acc)
+        for sign, t in terms[1:]:
+            acc = ('add' if sign > 0 else 'sub', acc, t)
+        if have_const and const != 0.0:
+            acc = ('add', acc, _const(const))
+        return acc
+
+    def mul(self, e: sp.Mul):
+        coef = 1.0
+        num: List[tuple] = []
+        den: List[tuple] = []
+        for f in e.args:
+            if f.is_Number and f.is_real:
+                coef *= _num_to_float(f)
+                continue
+            if f.is_Pow and f.exp.is_Integer and f.exp < 0:
+                n = -int(f.exp)
+                b = self.node(f.base)
+                den.append(b if n == 1 else self._pown(b, n))
+                continue
+            num.append(self.node(f))
+        num.sort(key=lambda n: -_need(n))
+        den.sort(key=lambda n: -_need(n))
+
+        def product(fs):
+            acc = fs[0]
+            for f in fs[1:]:
+                acc = ('mul', acc, f)
+            return acc
+        if num:
+            acc = product(num)
+            if den:
+                acc = ('div', acc, product(den))
+            if coef == -1.0:
+                acc = ('neg', acc)
+            elif coef != 1.0:
+                acc = ('mul', acc, _const(coef))
+            return acc
+        if den:
+            return ('div', _const(coef), product(den))
+        return _const(coef)
+
+    def _pown(self, b, n: int):
+        if n == 1:
+            return b
+        if n <= 16:
+            return ('pown', b, n)
+        return ('pow', b, float(n))
+
+    def pow(self, base: sp.Basic, ex: sp.Basic):
+        if ex.is_Integer:
+            n = int(ex)
+            if n == 0:
+                return _const(1.0)
+            b = self.node(base)
+            if n > 0:
+                return self._pown(b, n)
+            return ('div', _const(1.0), self._pown(b, -n))
+        if ex.is_Rational:
+            b = self.node(base)
+            if ex == sp.Rational(1, 2):
+                return ('sqrt', b)
+            return ('pow', b, _num_to_float(ex))
+        if ex.is_Number:
+            return ('pow', self.node(base), float(ex))
+        # general power: exp(ex * log(base))
+        return ('exp', ('mul', self.node(ex), ('log', self.node(base))))
+
+
+# --------------------------------------------------------------------------- Sethi-Ullman
+def _need(n) -> int:
+    """Stack slots needed to evaluate node n (fused leaf operands need none)."""
+    k = n[0]
+    if k in ('x', 'y', 'c', 'i'):
+        return 1
+    if k in ('neg', 'sqrt', 'exp', 'log', 'abs', 'pown', 'pow'):
+        return _need(n[1])
+    a, b = n[1], n[2]
+    if _is_leaf(b) and k in ('add', 'sub', 'mul', 'div'):
+        return _need(a)
+    if _is_leaf(a) and k in ('add', 'mul', 'sub') or (k == 'div' and a[0] == 'c'):
+        return _need(b)
+    na, nb = _need(a), _need(b)
+    if na == nb:
+        return na + 1
+    return max(na, nb)
+
+
+class _Emit:
+    def __init__(self):
+        self.w: List[int] = []
+        self.d = 0
+        self.dmax = 0
+
+    def op(self, name: str, imm: Optional[float] = None, arg: int = 0):
+        code = PDOP[name]
+        self.w.append(code | (arg << 8))
+        if code in HAS_IMM:
+            lo, hi = struct.unpack('<II', struct.pack('<d', float(imm)))
+            self.w.append(_s32(lo))
+            self.w.append(_s32(hi))
+        if name.startswith('PUSH'):
+            self.d += 1
+            self.dmax = max(self.dmax, self.d)
+        elif name in ('ADD', 'SUB', 'RSUB', 'MUL', 'DIV', 'RDIV'):
+            self.d -= 1
+
+    def leaf(self, n):
+        if n[0] == 'x':
+            self.op('PUSH_X')
+        elif n[0] == 'y':
+            self.op('PUSH_Y')
+        elif n[0] == 'i':
+            self.op('PUSH_I')
+        else:
+            self.op('PUSH_C', n[1])
+
+    def fused(self, k: str, leaf) -> bool:
+        """top = top (k) leaf as one opcode, if one exists."""
+        t = leaf[0]
+        if t == 'c':
+            c = leaf[1]
+            if k == 'add':
+                self.op('ADDC', c)
+            elif k == 'sub':
+                self.op('ADDC', -c)
+            elif k == 'mul':
+                if c == -1.0:
+                    self.op('NEG')
+                else:
+                    self.op('MULC', c)
+            elif k == 'div':
+                self.op('MULC', 1.0 / c)
+            return True
+        if t in ('x', 'y'):
+            ax = 'X' if t == 'x' else 'Y'
+            self.op({'add': 'ADD_', 'sub': 'SUB_', 'mul': 'MUL_', 'div': 'DIV_'}[k] + ax)
+            return True
+        return False
+
+    def emit(self, n):
+        k = n[0]
+        if k in ('x', 'y', 'c', 'i'):
+            self.leaf(n)
+            return
+        if k in ('neg', 'sqrt', 'exp', 'log', 'abs'):
+            self.emit(n[1])
+            self.op(k.upper())
+            return
+        if k == 'pown':
+            self.emit(n[1])
+            self.op('POWN', arg=n[2])
+            return
+        if k == 'pow':
+            self.emit(n[1])
+            self.op('POW', n[2])
+            return
+        a, b = n[1], n[2]
+        if _is_leaf(b) and k in ('add', 'sub', 'mul', 'div'):
+            self.emit(a)
+            self.fused(k, b)
+            return
+        if _is_leaf(a) and k in ('add', 'mul'):
+            self.emit(b)
+            self.fused(k, a)
+            return
+        if _is_leaf(a) and k == 'sub':          # leaf - b = -(b) + leaf
+            self.emit(b)
+            self.op('NEG')
+            self.fused('add', a)
+            return
+        if k == 'div' and a[0] == 'c':          # c / b
+            self.emit(b)
+            self.op('RDIVC', a[1])
+            return
+        na, nb = _need(a), _need(b)
+        if na >= nb:
+            self.emit(a)
+            self.emit(b)
+            self.op(k.upper())
+        else:
+            self.emit(b)
+            self.emit(a)
+            self.op({'add': 'ADD', 'mul': 'MUL', 'sub': 'RSUB', 'div': 'RDIV'}[k])
+
+
+def _s32(u: int) -> int:
+    return u - (1 << 32) if u >= (1 << 31) else u
+
+
+# --------------------------------------------------------------------------- public API
+def lower(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
+          consts: Optional[Dict[sp.Symbol, sp.Basic]] = None):
+    """SymPy tree -> IR node (raises Unsupported)."""
+    lw = _Lower(x_sym, y_sym, consts or {})
+    return lw.node(expr), lw.uses_i
+
+
+def _op_positions(body: Sequence[int]):
+    i = 0
+    while i < len(body):
+        yield i
+        i += 3 if (body[i] & 0xff) in HAS_IMM else 1
+
+
+def compile_ir(ir, uses_i: bool = False) -> List[int]:
+    em = _Emit()
+    em.emit(ir)
+    if em.d != 1:
+        raise AssertionError('stack imbalance in flattener')
+    if em.dmax > MAX_STACK:
+        raise Unsupported(f'stack depth {em.dmax} > {MAX_STACK}')
+    coord_ops = {PDOP[k] for k in ('PUSH_X', 'PUSH_Y', 'ADD_X', 'ADD_Y', 'SUB_X', 'SUB_Y',
+                                   'MUL_X', 'MUL_Y', 'DIV_X', 'DIV_Y')}
+    has_coord = any(em.w[i] & 0xff in coord_ops for i in _op_positions(em.w))
+    hdr = (PDOP['HEADER'] | (em.dmax << 8) | (FLAG_COMPLEX if uses_i else 0)
+           | (0 if has_coord else FLAG_NOCOORD))
+    return [hdr] + em.w
+
+
+def flatten(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
+            consts: Optional[Dict[sp.Symbol, sp.Basic]] = None) -> List[int]:
+    """SymPy expression -> program words (header first).  Raises Unsupported."""
+    ir, uses_i = lower(expr, x_sym, y_sym, consts)
+    return compile_ir(ir, uses_i)
+
+
+def program_depth(words: Sequence[int]) -> int:
+    return (words[0] >> 8) & 0xff
+
+
+def disasm(words: Sequence[int]) -> str:
+    from .opcodes import OP_NAME
+    out = [f'HEADER depth={program_depth(words)} flags={words[0] >> 16:#x}']
+    i = 1
+    while i < len(words):
+        w = words[i] & 0xffffffff
+        op = w & 0xff
+        name = OP_NAME.get(op, f'?{op}')
+        if op in HAS_IMM:
+            lo, hi = words[i + 1] & 0xffffffff, words[i + 2] & 0xffffffff
+            v = struct.unpack('<d', struct.pack('<II', lo, hi))[0]
+            out.append(f'{name} {v!r}')
+            i += 3
+        else:
+            out.append(f'{name}' + (f' {w >> 8}' if op == PDOP['POWN'] else ''))
+            i += 1
+    return '\n'.join(out)
+
+
+def pack(programs: Sequence[Sequence[int]]):
+    """List of programs -> (ops int32 array, offsets int64 array)."""
+    import numpy as np
+    lens = np.fromiter((len(p) for p in programs), dtype=np.int64, count=len(programs))
+    offsets = np.zeros(len(programs) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    ops = np.empty(int(offsets[-1]), dtype=np.int32)
+    for i, p in enumerate(programs):
+        ops[offsets[i]:offsets[i + 1]] = p
+    return ops, offsets

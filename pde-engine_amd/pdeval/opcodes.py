@@ -1,0 +1,35 @@
+"""Opcode numbers of the candidate-program format; mirror of ``include/pdeval.h``.
+
+``tests/test_abi.py`` parses the header and checks every value here against it.
+"""
+
+PDOP = dict(
+    HEADER=0,
+    PUSH_X=1, PUSH_Y=2, PUSH_C=3,
+    ADD=4, SUB=5, RSUB=6, MUL=7, DIV=8, RDIV=9,
+    ADDC=10, MULC=11, RDIVC=12, NEG=13,
+    ADD_X=14, ADD_Y=15, MUL_X=16, MUL_Y=17, SUB_X=18, SUB_Y=19,
+    POWN=20, POW=21, EXP=22, LOG=23, ABS=24, SQRT=25,
+    DIV_X=26, DIV_Y=27, PUSH_I=28, UNSUPPORTED=254,
+)
+OP_NAME = {v: k for k, v in PDOP.items()}
+HAS_IMM = {PDOP['PUSH_C'], PDOP['ADDC'], PDOP['MULC'], PDOP['RDIVC'], PDOP['POW']}
+
+PROBLEM_FORCE_FREE = 0
+PROBLEM_KERR = 1
+
+# per-candidate classes (status[] output)
+CLS_ACCEPT = 0
+CLS_REJECT_POINT = 1
+CLS_REJECT_GRID = 2
+CLS_ZERO_GRADIENT = 3
+CLS_NONFINITE_REF = 4
+CLS_UNSUPPORTED = 5
+CLS_BAD_PROGRAM = 6
+CLS_NAME = {0: 'accept', 1: 'reject_point', 2: 'reject_grid', 3: 'zero_gradient',
+            4: 'nonfinite_ref', 5: 'unsupported', 6: 'bad_program'}
+
+MAX_STACK = 8
+FP_N = 4
+FLAG_COMPLEX = 1 << 16   # header flag: program pushes the imaginary unit
+FLAG_NOCOORD = 1 << 17   # header flag: program references no coordinate

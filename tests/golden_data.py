@@ -1,0 +1,29 @@
+"""Loaders for the committed golden fixtures (tests/golden/)."""
+import gzip
+import json
+import os
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
+
+
+def ref_rows(*names):
+    rows = []
+    for n in names:
+        with open(os.path.join(GOLDEN, 'ref', n)) as f:
+            rows.extend(json.loads(l) for l in f)
+    return rows
+
+
+def decided(rows):
+    """Rows with a reference verdict (no timeout, no validator error)."""
+    return [r for r in rows if not r.get('timeout') and r.get('ok') is not None]
+
+
+def stream(name, with_index=False):
+    with gzip.open(os.path.join(GOLDEN, 'streams', name), 'rt') as f:
+        rows = [l.rstrip('\n').split('\t') for l in f]
+    return rows
+
+
+FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl')
+KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl')

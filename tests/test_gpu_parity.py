@@ -1,0 +1,68 @@
+"""GPU parity: libpdeval.so on the MI355X vs the CPU oracle and vs the reference's verdicts.
+
+Bar (north star): accept/reject verdicts identical to the reference's on every fixture the
+reference decided; residuals at the reference point(s) within 1e-10 relative of the oracle's
+(absolute floor 1e-13 * S for residuals that are rounding noise of an exact zero).
+"""
+import numpy as np
+import pytest
+
+import golden_data as G
+import oracle_lib as O
+from pdeval import problem_defs as P
+from pdeval._lib import Context
+
+pytestmark = pytest.mark.gpu
+
+REL_TOL = 1e-10
+EPS = 2.0 ** -52
+
+
+def check_residuals(dev, ora, strings, tau=1e-10):
+    """Residual at the reference point(s).  Point-stage rejects (q > tau): the device value
+    agrees with the oracle's to 1e-10 relative -- or, where the residual itself is the result
+    of cancellation, to the fp64 conditioning limit 64 eps / q (neither side is exact there).
+    Point-stage passes: the residual is rounding noise of an exact zero; both must be noise
+    (q <= tau), which the equal statuses already assert."""
+    q = np.asarray(ora['q_ref'])
+    d, o = dev['res_ref'], ora['res_ref']
+    for i in range(len(q)):
+        if not (q[i] > tau) or not np.all(np.isfinite(o[i])):
+            continue
+        tol = max(REL_TOL, 64 * EPS / q[i]) if dev['res_ref'].shape[1] == 1 else REL_TOL
+        err = np.max(np.abs(d[i] - o[i]) / np.maximum(np.abs(o[i]), 1e-300))
+        assert err <= tol, (strings[i], d[i], o[i], err, tol)
+
+
+@pytest.fixture(scope='module')
+def ff_ctx():
+    return Context(0)
+
+
+def _cmp_device_oracle(ctx, pd_, strings):
+    ops, off, _ = P.compile_strings(pd_, strings)
+    dev = ctx.validate(ops, off)
+    ora = O.validate(pd_.problem_id, ops, off)
+    assert np.array_equal(dev['status'], ora['status']), \
+        [(s, int(a), int(b)) for s, a, b in zip(strings, dev['status'], ora['status']) if a != b][:10]
+    assert np.array_equal(dev['n_bad'], ora['n_bad'])
+    assert np.array_equal(dev['n_nonfinite'], ora['n_nonfinite'])
+    check_residuals(dev, ora, strings)
+    return dev, ora
+
+
+def test_known_solutions_ff(ff_ctx):
+    pd_ = P.force_free()
+    dev, _ = _cmp_device_oracle(ff_ctx, pd_, list(pd_.known_solutions))
+    assert dev['verdict'].all(), dev['status']
+
+
+def test_ff_reference_verdicts(ff_ctx):
+    pd_ = P.force_free()
+    rows = G.decided(G.ref_rows(*G.FF_REF))
+    dev, _ = _cmp_device_oracle(ff_ctx, pd_, [r['expr'] for r in rows])
+    ref = np.array([bool(r['ok']) for r in rows])
+    mism = [(r['expr'], r['reason'], int(s)) for r, v, s in zip(rows, dev['verdict'], dev['status'])
+            if bool(v) != bool(r['ok'])]
+    assert not mism, mism[:10]
+    assert (dev['verdict'] == ref).all()
