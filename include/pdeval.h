@@ -49,6 +49,11 @@ extern "C" {
 #define PDEVAL_CLS_NONFINITE_REF   4   /* non-finite at a reference point in real arithmetic */
 #define PDEVAL_CLS_UNSUPPORTED     5   /* program uses an opcode this build does not handle */
 #define PDEVAL_CLS_BAD_PROGRAM     6   /* malformed program (stack under/overflow)          */
+#define PDEVAL_CLS_REJECT_SYMBOLIC 7   /* zero on the grid, but non-smooth (Abs) in both
+                                          coordinates: the reference's symbolic stage cannot
+                                          prove it (assumptions are lost in its string round
+                                          trip, validator.py:242-252 / lean_bridge.py:73), so
+                                          with strict_symbolic it is rejected as there     */
 
 /* ---- opcodes (bits 0-7 of a program word) ---- */
 enum pdeval_opcode {
@@ -90,6 +95,10 @@ enum pdeval_opcode {
 /* Program header word: opcode 0 | stack depth << 8 | flags */
 #define PDEVAL_FLAG_COMPLEX  (1u << 16)  /* pushes the imaginary unit: complex pass only   */
 #define PDEVAL_FLAG_NOCOORD  (1u << 17)  /* references no coordinate (u is a constant)   */
+#define PDEVAL_FLAG_RATIONAL (1u << 18)  /* rational operations and constants only: the
+                                            residual at a rational point is rational (host
+                                            reason strings, validator.py:371-380)      */
+#define PDEVAL_FLAG_NONSMOOTH2D (1u << 19) /* contains Abs and references both coordinates */
 
 /* Thresholds of the scaled zero test (DESIGN.md "Zero test"). */
 typedef struct pdeval_params {
@@ -100,6 +109,9 @@ typedef struct pdeval_params {
                             0: stop after the point stage for point-rejects (as the
                                reference does, validator.py:371-402)                 */
     int32_t max_bad;     /* grid stage rejects iff n_bad > max_bad                   */
+    int32_t strict_symbolic; /* 1: reproduce the reference's symbolic-stage verdict on
+                                non-smooth candidates (PDEVAL_CLS_REJECT_SYMBOLIC)       */
+    int32_t reserved;
 } pdeval_params;
 
 /* Per-candidate outputs; any pointer may be NULL (not produced).  Host or device memory

@@ -188,6 +188,8 @@ extern "C" int pdeval_default_params(int problem_id, pdeval_params* p) {
     p->kerr_abs_tol = 1e-10;  // kerr validator.py:190
     p->full_grid = 1;
     p->max_bad = 0;
+    p->strict_symbolic = 1;
+    p->reserved = 0;
     (void)problem_id;
     return PDEVAL_OK;
 }

@@ -611,6 +611,8 @@ __global__ __launch_bounds__(256, 2) void validate_kernel(KernelArgs a) {
                 if (!any_grad && nfin > 0 && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
                 else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;
                 else if (nbad > a.prm.max_bad) cls = PDEVAL_CLS_REJECT_GRID;
+                else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic &&
+                         (hdr & PDEVAL_FLAG_NONSMOOTH2D)) cls = PDEVAL_CLS_REJECT_SYMBOLIC;
                 else cls = PDEVAL_CLS_ACCEPT;
             }
             if (a.out.status) a.out.status[cand] = (uint8_t)cls;

@@ -27,7 +27,8 @@ EXPORTS = (
 
 class Params(C.Structure):
     _fields_ = [('tau_point', C.c_double), ('tau_grid', C.c_double),
-                ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32)]
+                ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32),
+                ('strict_symbolic', C.c_int32), ('reserved', C.c_int32)]
 
 
 class Outputs(C.Structure):

@@ -1,0 +1,151 @@
+"""Batch validation with the reference's verdict semantics.
+
+``BatchValidator.validate_exprs`` is the batched replacement for calling
+``validator.validate(u, check_regularity=False, fast_point_only=False, lean_first=True,
+defer_heavy_checks=True, enforce_anchor=False)`` once per candidate
+(``general_method_paper_reproduction.py:1299-1316`` inline, ``:1768-1782`` worker).  One call
+flattens every tree on the host, sends the whole batch through libpdeval.so, and maps each
+candidate's class to the reference's ``(bool, reason)`` strings:
+
+force-free (``problems/force_free/validator.py``)
+  zero gradient  -> (False, "Zero gradient (constant expression)")                  :309-312
+  point reject   -> (False, "Invalid (point check != 0)") for a rational det at p*,  :371-380
+                    (False, "Invalid (point check ≈ {|det|:.2e})") otherwise        :388-397
+  grid reject    -> (False, "Invalid (Lean could not simplify det to 0 symbolically)") :414-416
+  accept         -> (True,  "Valid foliation (Lean: det = 0 symbolically)")           :410-413
+Kerr (``problems/kerr_magnetosphere/validator.py``)
+  zero gradient  -> (False, "Trivial constant solution excluded")                     :231-240
+  point reject   -> (False, "PDE residual != 0 (fast point check) | residual: ...")  :264-269
+  grid reject    -> (False, "PDE residual != 0 | residual: ...")                     :308-315
+  accept         -> (True,  "Valid (exact zero; heavy checks deferred)")              :318-323
+The residual text after "residual:" is numeric here (the reference prints a symbolic
+numerator/denominator, which is not reproduced).
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import sympy as sp
+
+from . import problem_defs as P
+from .flatten import Unsupported
+from .opcodes import (CLS_ACCEPT, CLS_BAD_PROGRAM, CLS_NONFINITE_REF, CLS_REJECT_GRID,
+                      CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC, CLS_UNSUPPORTED, CLS_ZERO_GRADIENT, FLAG_RATIONAL,
+                      PROBLEM_FORCE_FREE)
+
+
+@dataclass
+class Verdict:
+    ok: bool
+    reason: str
+    cls: int
+    q_ref: float
+    res_ref: Tuple[float, ...]
+    q_grid: float
+    n_bad: int
+    n_nonfinite: int
+    fingerprint: Tuple[float, ...]
+
+
+def _fmt_point(v: float) -> str:
+    return f'Invalid (point check ≈ {abs(v):.2e})'
+
+
+def reason_for(problem_id: int, cls: int, res_ref: Sequence[float], q_ref: float,
+               q_grid: float, rational: bool, note: Optional[str] = None) -> Tuple[bool, str]:
+    if problem_id == PROBLEM_FORCE_FREE:
+        if cls == CLS_ACCEPT:
+            return True, 'Valid foliation (Lean: det = 0 symbolically)'
+        if cls == CLS_REJECT_POINT:
+            if not np.isfinite(res_ref[0]):
+                return False, 'Invalid (point check != 0)'
+            return False, 'Invalid (point check != 0)' if rational else _fmt_point(res_ref[0])
+        if cls in (CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC):
+            return False, 'Invalid (Lean could not simplify det to 0 symbolically)'
+        if cls == CLS_ZERO_GRADIENT:
+            return False, 'Zero gradient (constant expression)'
+        if cls == CLS_NONFINITE_REF:
+            return False, 'Could not evaluate point check'
+    else:
+        if cls == CLS_ACCEPT:
+            return True, 'Valid (exact zero; heavy checks deferred)'
+        if cls == CLS_REJECT_POINT:
+            return False, (f'PDE residual != 0 (fast point check) | residual: '
+                           f'max|lhs| at test points ≈ {q_ref:.3e}')
+        if cls == CLS_REJECT_GRID:
+            return False, f'PDE residual != 0 | residual: max scaled |lhs| on grid ≈ {q_grid:.3e}'
+        if cls == CLS_ZERO_GRADIENT:
+            return False, 'Trivial constant solution excluded'
+        if cls == CLS_NONFINITE_REF:
+            return False, 'Invalid (non-real at test point)'
+    if cls == CLS_UNSUPPORTED:
+        return False, f'Error: unsupported construct ({note or "opcode"})'
+    return False, 'Error: malformed program'
+
+
+class BatchValidator:
+    """One problem on one GPU.  Thread-safe (calls are serialized per context)."""
+
+    def __init__(self, problem: str = 'force_free', device: int = 0, params=None):
+        from ._lib import Context, default_params
+        self.pd = P.get(problem)
+        self.device = device
+        self.ctx = Context(self.pd.problem_id, device=device)
+        self.params = params if params is not None else default_params(self.pd.problem_id)
+        self._lock = threading.Lock()
+
+    @property
+    def problem_id(self) -> int:
+        return self.pd.problem_id
+
+    def compile(self, exprs: Sequence[sp.Basic]):
+        return P.compile_exprs(self.pd, exprs)
+
+    def run(self, ops, offsets):
+        with self._lock:
+            return self.ctx.validate(ops, offsets, self.params)
+
+    def validate_exprs(self, exprs: Sequence[sp.Basic]) -> List[Verdict]:
+        if not exprs:
+            return []
+        ops, off, notes = self.compile(exprs)
+        r = self.run(ops, off)
+        out = []
+        for i in range(len(exprs)):
+            hdr = int(ops[off[i]])
+            ok, reason = reason_for(self.problem_id, int(r['status'][i]), r['res_ref'][i],
+                                    float(r['q_ref'][i]), float(r['q_grid'][i]),
+                                    bool(hdr & FLAG_RATIONAL), notes[i])
+            out.append(Verdict(ok, reason, int(r['status'][i]), float(r['q_ref'][i]),
+                               tuple(float(v) for v in r['res_ref'][i]), float(r['q_grid'][i]),
+                               int(r['n_bad'][i]), int(r['n_nonfinite'][i]),
+                               tuple(float(v) for v in r['fingerprint'][i])))
+        return out
+
+    def validate_strings(self, strings: Sequence[str]) -> List[Verdict]:
+        exprs = []
+        for s in strings:
+            try:
+                exprs.append(self.pd.parse(s))
+            except Exception:   # noqa: BLE001
+                exprs.append(sp.Function('unparsable')(self.pd.x))
+        return self.validate_exprs(exprs)
+
+    def close(self):
+        self.ctx.close()
+
+
+_VALIDATORS: Dict[Tuple[str, int], BatchValidator] = {}
+_VLOCK = threading.Lock()
+
+
+def get_validator(problem: str, device: int = 0) -> BatchValidator:
+    """Process-wide BatchValidator per (problem, device): one libpdeval context per GPU."""
+    key = (P.get(problem).slug, device)
+    with _VLOCK:
+        if key not in _VALIDATORS:
+            _VALIDATORS[key] = BatchValidator(problem, device)
+        return _VALIDATORS[key]

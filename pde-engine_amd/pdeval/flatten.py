@@ -27,7 +27,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import sympy as sp
 
-from .opcodes import PDOP, HAS_IMM, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD
+from .opcodes import (PDOP, HAS_IMM, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD, FLAG_RATIONAL,
+                      FLAG_NONSMOOTH2D)
 
 
 class Unsupported(Exception):
@@ -61,6 +62,7 @@ class _Lower:
         self.y = y_sym
         self.consts = consts
         self.uses_i = False
+        self.irrational_const = False
 
     def node(self, e: sp.Basic):
         if e.is_Symbol:
@@ -75,10 +77,14 @@ class _Lower:
         if e is sp.nan or e is sp.zoo or e is sp.oo or e is sp.S.NegativeInfinity:
             return _const(float('nan'))     # the driver's pre-validate filter drops these
         if e.is_Number:
+            if not e.is_Rational:
+                self.irrational_const = True
             return _const(_num_to_float(e))
         if e is sp.E:
+            self.irrational_const = True
             return _const(math.e)
         if e is sp.pi:
+            self.irrational_const = True
             return _const(math.pi)
         if e is sp.I:
             self.uses_i = True
@@ -311,9 +317,15 @@ def _s32(u: int) -> int:
 # --------------------------------------------------------------------------- public API
 def lower(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
           consts: Optional[Dict[sp.Symbol, sp.Basic]] = None):
-    """SymPy tree -> IR node (raises Unsupported)."""
+    """SymPy tree -> IR node (raises Unsupported).  Returns (ir, uses_i, rational_consts)."""
     lw = _Lower(x_sym, y_sym, consts or {})
-    return lw.node(expr), lw.uses_i
+    return lw.node(expr), lw.uses_i, not lw.irrational_const
+
+
+_RATIONAL_OPS = {PDOP[k] for k in ('PUSH_X', 'PUSH_Y', 'PUSH_C', 'ADD', 'SUB', 'RSUB', 'MUL', 'DIV',
+                                   'RDIV', 'ADDC', 'MULC', 'RDIVC', 'NEG', 'ADD_X', 'ADD_Y',
+                                   'MUL_X', 'MUL_Y', 'SUB_X', 'SUB_Y', 'DIV_X', 'DIV_Y', 'POWN',
+                                   'ABS')}
 
 
 def _op_positions(body: Sequence[int]):
@@ -323,7 +335,7 @@ def _op_positions(body: Sequence[int]):
         i += 3 if (body[i] & 0xff) in HAS_IMM else 1
 
 
-def compile_ir(ir, uses_i: bool = False) -> List[int]:
+def compile_ir(ir, uses_i: bool = False, rational_consts: bool = True) -> List[int]:
     em = _Emit()
     em.emit(ir)
     if em.d != 1:
@@ -333,16 +345,23 @@ def compile_ir(ir, uses_i: bool = False) -> List[int]:
     coord_ops = {PDOP[k] for k in ('PUSH_X', 'PUSH_Y', 'ADD_X', 'ADD_Y', 'SUB_X', 'SUB_Y',
                                    'MUL_X', 'MUL_Y', 'DIV_X', 'DIV_Y')}
     has_coord = any(em.w[i] & 0xff in coord_ops for i in _op_positions(em.w))
+    ops = [em.w[i] & 0xff for i in _op_positions(em.w)]
+    xs = any(o in (PDOP['PUSH_X'], PDOP['ADD_X'], PDOP['SUB_X'], PDOP['MUL_X'], PDOP['DIV_X']) for o in ops)
+    ys = any(o in (PDOP['PUSH_Y'], PDOP['ADD_Y'], PDOP['SUB_Y'], PDOP['MUL_Y'], PDOP['DIV_Y']) for o in ops)
+    nonsmooth2d = xs and ys and PDOP['ABS'] in ops
+    rational = rational_consts and not uses_i and all(
+        (em.w[i] & 0xff) in _RATIONAL_OPS for i in _op_positions(em.w))
     hdr = (PDOP['HEADER'] | (em.dmax << 8) | (FLAG_COMPLEX if uses_i else 0)
-           | (0 if has_coord else FLAG_NOCOORD))
+           | (0 if has_coord else FLAG_NOCOORD) | (FLAG_RATIONAL if rational else 0)
+           | (FLAG_NONSMOOTH2D if nonsmooth2d else 0))
     return [hdr] + em.w
 
 
 def flatten(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
             consts: Optional[Dict[sp.Symbol, sp.Basic]] = None) -> List[int]:
     """SymPy expression -> program words (header first).  Raises Unsupported."""
-    ir, uses_i = lower(expr, x_sym, y_sym, consts)
-    return compile_ir(ir, uses_i)
+    ir, uses_i, rational_consts = lower(expr, x_sym, y_sym, consts)
+    return compile_ir(ir, uses_i, rational_consts)
 
 
 def program_depth(words: Sequence[int]) -> int:

@@ -26,10 +26,13 @@ CLS_ZERO_GRADIENT = 3
 CLS_NONFINITE_REF = 4
 CLS_UNSUPPORTED = 5
 CLS_BAD_PROGRAM = 6
+CLS_REJECT_SYMBOLIC = 7
 CLS_NAME = {0: 'accept', 1: 'reject_point', 2: 'reject_grid', 3: 'zero_gradient',
-            4: 'nonfinite_ref', 5: 'unsupported', 6: 'bad_program'}
+            4: 'nonfinite_ref', 5: 'unsupported', 6: 'bad_program', 7: 'reject_symbolic'}
 
 MAX_STACK = 8
 FP_N = 4
 FLAG_COMPLEX = 1 << 16   # header flag: program pushes the imaginary unit
 FLAG_NOCOORD = 1 << 17   # header flag: program references no coordinate
+FLAG_RATIONAL = 1 << 18  # header flag: value is rational at rational points (exact det)
+FLAG_NONSMOOTH2D = 1 << 19  # header flag: contains Abs and references both coordinates

@@ -66,3 +66,44 @@ def test_ff_reference_verdicts(ff_ctx):
             if bool(v) != bool(r['ok'])]
     assert not mism, mism[:10]
     assert (dev['verdict'] == ref).all()
+
+
+@pytest.fixture(scope='module')
+def kerr_ctx():
+    return Context(1)
+
+
+def test_ff_edge_cases(ff_ctx):
+    pd_ = P.force_free()
+    rows = G.decided(G.ref_rows('ff_edge.jsonl'))
+    dev, _ = _cmp_device_oracle(ff_ctx, pd_, [r['expr'] for r in rows])
+    mism = [(r['expr'], r['reason'], int(s)) for r, v, s in zip(rows, dev['verdict'], dev['status'])
+            if bool(v) != bool(r['ok'])]
+    assert not mism, mism
+
+
+def test_kerr_reference_verdicts(kerr_ctx):
+    pd_ = P.kerr()
+    rows = G.decided(G.ref_rows(*G.KERR_REF, 'kerr_edge.jsonl'))
+    dev, _ = _cmp_device_oracle(kerr_ctx, pd_, [r['expr'] for r in rows])
+    mism = [(r['expr'], r['reason'][:60], int(s)) for r, v, s in zip(rows, dev['verdict'], dev['status'])
+            if bool(v) != bool(r['ok'])]
+    assert not mism, mism[:10]
+
+
+def test_plugin_api_reasons():
+    """The drop-in problems/ package answers with the reference's (bool, reason) pairs."""
+    from problems import load_problem
+    rows = G.decided(G.ref_rows(*G.FF_REF, 'ff_edge.jsonl'))
+    prob = load_problem('force_free')
+    locs = {**prob.symbols, **prob.constants, **prob.unary_ops}
+    import sympy as sp
+    us = [sp.sympify(r['expr'], locals=locs) for r in rows]
+    got = prob.validator.validate_batch(us, check_regularity=False, fast_point_only=False)
+    verdicts = sum(g[0] == r['ok'] for g, r in zip(got, rows))
+    cls = sum(g[1].split('≈')[0] == r['reason'].split('≈')[0] for g, r in zip(got, rows))
+    assert verdicts == len(rows)
+    assert cls >= 0.95 * len(rows), (cls, len(rows))
+    # the per-candidate contract of problems/__init__.py:52
+    assert prob.validator.validate(us[0], check_regularity=False) == got[0]
+    assert all(prob.validator.validate_known_solutions().values())
