@@ -1,0 +1,176 @@
+"""Validator worker pool -- the batched, GPU-backed ``_parallel_validator_worker``.
+
+Reproduces the INTENDED semantics of ``general_method_paper_reproduction.py:1671-1824`` (the
+snapshot's worker dies on a broken import):
+
+* input  : ``(expr_id, expr_str)`` tuples from ``task_queue`` (``None`` = shut down), or, when the
+           queue is idle, up to 50 ``pending`` rows claimed from the run table with the
+           compare-and-set ``UPDATE ... WHERE id=? AND validation_status='pending'`` (:1736-1751);
+* parse  : ``sympify(expr_str, locals=UNARY_OPS + symbols + constants)`` (:1703-1714, :1767);
+* verdict: ``problem.validator.validate_batch(us, **kwargs)`` with the kwargs of :1768-1782
+           filtered by the validator's signature -- one GPU call per batch instead of one
+           SymPy ``validate`` per candidate;
+* tagging: valid rows are matched against ``problem.known_solutions`` (:1783-1798): a grid
+           fingerprint pre-filter on the device, then the reference's ``simplify(u - known)
+           == 0`` on the host for fingerprint hits only;
+* output : ``(run_id, pid, 'start', expr_id, snippet[:120])`` and ``(run_id, pid, 'end',
+           [(status, is_valid, reason, is_paper, paper_name, expr_id), ...])`` on
+           ``result_queue`` (:1764, :1816), the protocol ``_db_update_writer`` consumes.
+"""
+from __future__ import annotations
+
+import inspect
+import os
+import queue as _queue
+import sqlite3
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import sympy as sp
+
+BASE_KWARGS = {'check_regularity': False, 'fast_point_only': False, 'lean_first': True,
+               'defer_heavy_checks': True, 'enforce_anchor': False}
+
+
+def filtered_kwargs(validator) -> Dict[str, object]:
+    try:
+        fn = getattr(validator, 'validate_batch', None) or validator.validate
+        allowed = set(inspect.signature(fn).parameters)
+        return {k: v for k, v in BASE_KWARGS.items() if k in allowed}
+    except (TypeError, ValueError):
+        return {'check_regularity': False, 'fast_point_only': False}
+
+
+class KnownSolutionTagger:
+    """Fingerprint pre-filter + exact SymPy confirmation of known-solution matches."""
+
+    def __init__(self, problem, locals_: Dict[str, object], device: int = 0, rtol: float = 1e-9):
+        from .batch import get_validator
+        self.known = []
+        self.locals = locals_
+        self.rtol = rtol
+        items = list((getattr(problem, 'known_solutions', None) or {}).items())
+        if not items:
+            self.fps = np.zeros((0, 4))
+            return
+        self.bv = get_validator(problem.slug, device)
+        exprs = [sp.sympify(k, locals=locals_) for k, _ in items]
+        res = self.bv.validate_exprs(exprs)
+        self.known = [(e, name) for e, (_, name) in zip(exprs, items)]
+        self.fps = np.array([v.fingerprint for v in res])
+
+    def fingerprints(self, us: Sequence[sp.Basic]) -> np.ndarray:
+        return np.array([v.fingerprint for v in self.bv.validate_exprs(list(us))])
+
+    def tag(self, us: Sequence[sp.Basic]) -> List[Tuple[bool, Optional[str]]]:
+        out: List[Tuple[bool, Optional[str]]] = [(False, None)] * len(us)
+        if not self.known or not len(us):
+            return out
+        fp = self.fingerprints(us)
+        for i, u in enumerate(us):
+            for k, (ke, name) in enumerate(self.known):
+                a, b = fp[i], self.fps[k]
+                fin = np.isfinite(a) & np.isfinite(b)
+                if fin.sum() < 2 or not np.allclose(a[fin], b[fin], rtol=self.rtol, atol=1e-12):
+                    continue
+                try:
+                    if sp.simplify(u - ke) == 0:        # the reference's test, :1791
+                        out[i] = (True, name)
+                        break
+                except Exception:   # noqa: BLE001
+                    pass
+        return out
+
+
+def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[str],
+                     problem_name: str = 'force_free', task_queue=None, result_queue=None,
+                     batch_size: int = 4096, device: int = 0, idle_exit_s: Optional[float] = None):
+    """Worker process body (one per GPU).  Returns the number of candidates validated."""
+    from problems import load_problem
+    problem = load_problem(problem_name)
+    validator = problem.validator
+    if hasattr(validator, 'device'):
+        validator.device = device
+    locs: Dict[str, object] = {}
+    locs.update(problem.unary_ops)
+    locs.update(problem.symbols)
+    locs.update(problem.constants)
+    kwargs = filtered_kwargs(validator)
+    tagger = KnownSolutionTagger(problem, locs, device)
+    conn = None
+    if db_path and table_name:
+        conn = sqlite3.connect(db_path)
+        conn.execute('PRAGMA journal_mode=WAL')
+        conn.execute('PRAGMA busy_timeout=5000')
+    pid = os.getpid()
+    done = 0
+    stop = False
+    last_work = time.time()
+    while not stop:
+        claimed: List[Tuple[int, str]] = []
+        if task_queue is not None:
+            try:
+                item = task_queue.get(timeout=0.2)
+                if item is None:
+                    stop = True
+                else:
+                    claimed.append(item)
+                    while len(claimed) < batch_size:
+                        item = task_queue.get_nowait()
+                        if item is None:
+                            stop = True
+                            break
+                        claimed.append(item)
+            except _queue.Empty:
+                pass
+        if not claimed and conn is not None and not stop:
+            cur = conn.execute(f"SELECT id, expression FROM {table_name} "
+                               f"WHERE validation_status = 'pending' LIMIT 50")
+            for expr_id, expr_str in cur.fetchall():
+                c2 = conn.execute(f"UPDATE {table_name} SET validation_status = 'in_progress' "
+                                  f"WHERE id = ? AND validation_status = 'pending'", (expr_id,))
+                if c2.rowcount == 1:
+                    claimed.append((expr_id, expr_str))
+            conn.commit()
+        if not claimed:
+            if idle_exit_s is not None and time.time() - last_work > idle_exit_s:
+                break
+            if not stop:
+                time.sleep(0.2)
+            continue
+        last_work = time.time()
+        if result_queue is not None:
+            try:
+                result_queue.put((run_id, pid, 'start', claimed[0][0], claimed[0][1][:120]), timeout=0.5)
+            except Exception:   # noqa: BLE001
+                pass
+        results = process_batch(claimed, validator, kwargs, locs, tagger)
+        done += len(results)
+        if result_queue is not None:
+            result_queue.put((run_id, pid, 'end', results), timeout=5.0)
+    if conn is not None:
+        conn.close()
+    return done
+
+
+def process_batch(claimed, validator, kwargs, locs, tagger):
+    """(expr_id, expr_str) list -> result tuples of the reference's writer protocol."""
+    us, ids, results = [], [], []
+    for expr_id, expr_str in claimed:
+        try:
+            us.append(sp.sympify(expr_str, locals=locs))
+            ids.append(expr_id)
+        except Exception as e:   # noqa: BLE001
+            results.append(('error', None, f'Validator Error: {e}', None, None, expr_id))
+    if us:
+        if hasattr(validator, 'validate_batch'):
+            verdicts = validator.validate_batch(us, **kwargs)
+        else:
+            verdicts = [validator.validate(u, **kwargs) for u in us]
+        valid = [i for i, (ok, _) in enumerate(verdicts) if ok]
+        tags = dict(zip(valid, tagger.tag([us[i] for i in valid])))
+        for i, (ok, reason) in enumerate(verdicts):
+            is_paper, name = tags.get(i, (False, None))
+            results.append(('completed', bool(ok), reason, is_paper, name, ids[i]))
+    return results
