@@ -26,14 +26,17 @@ struct pdeval_ctx {
     int n_ref = 0, n_pts = 0;
     int fp_pts[PDEVAL_FP_N] = {0, 0, 0, 0};
     hipStream_t stream = nullptr;
-    double* d_px = nullptr;
-    double* d_py = nullptr;
+    double ref_x[4] = {0, 0, 0, 0}, ref_y[4] = {0, 0, 0, 0};
+    int nx = 0, ny = 0;
+    double* d_gx = nullptr;   // nx grid abscissae
+    double* d_gy = nullptr;   // ny grid ordinates
     double* d_kc = nullptr;
     // scratch: work lists and their counters
     int64_t cap = 0;
-    int64_t* d_defer = nullptr;
+    int64_t* d_defer = nullptr;   // pass 1 -> pass 2 (stack 3..4)
+    int64_t* d_defer2 = nullptr;  // pass 2 -> pass 3 (stack 5..8)
     int64_t* d_cplx = nullptr;
-    int32_t* d_counts = nullptr;  // [0] defer, [1] cplx
+    int32_t* d_counts = nullptr;  // [0] defer, [1] cplx, [2] defer2
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -109,7 +112,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     Grid g = default_grid(problem_id);
     if (grid && n_grid >= 8) std::memcpy(&g, grid, sizeof(Grid));
     const int nx = (int)g.nx, ny = (int)g.ny;
-    if (nx <= 0 || ny <= 0 || nx * ny > (1 << 22)) {
+    if (nx <= 0 || ny <= 0 || ny % 64 != 0 || nx * ny > (1 << 22)) {
         delete c;
         g_err = "pdeval_create: bad grid";
         return PDEVAL_ERR_ARG;
@@ -125,11 +128,20 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
         py = {0.6, 1.0 / 3.0, -0.4};
     }
     c->n_ref = (int)px.size();
+    for (int k = 0; k < c->n_ref; ++k) {
+        c->ref_x[k] = px[k];
+        c->ref_y[k] = py[k];
+    }
+    std::vector<double> gx(nx), gy(ny);
+    for (int i = 0; i < nx; ++i) gx[i] = g.x_lo + (i + g.x_ph) * ((g.x_hi - g.x_lo) / nx);
+    for (int j = 0; j < ny; ++j) gy[j] = g.y_lo + (j + g.y_ph) * ((g.y_hi - g.y_lo) / ny);
     for (int i = 0; i < nx; ++i)
         for (int j = 0; j < ny; ++j) {
-            px.push_back(g.x_lo + (i + g.x_ph) * ((g.x_hi - g.x_lo) / nx));
-            py.push_back(g.y_lo + (j + g.y_ph) * ((g.y_hi - g.y_lo) / ny));
+            px.push_back(gx[i]);
+            py.push_back(gy[j]);
         }
+    c->nx = nx;
+    c->ny = ny;
     c->n_pts = (int)px.size();
     const int G = nx * ny;
     c->fp_pts[0] = 0;
@@ -148,11 +160,12 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if ((e = hipSetDevice(device_id)) != hipSuccess) return fail("hipSetDevice", e);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
-    const size_t pb = px.size() * sizeof(double);
-    if ((e = hipMalloc(&c->d_px, pb)) != hipSuccess) return fail("hipMalloc", e);
-    if ((e = hipMalloc(&c->d_py, pb)) != hipSuccess) return fail("hipMalloc", e);
-    if ((e = hipMemcpy(c->d_px, px.data(), pb, hipMemcpyHostToDevice)) != hipSuccess) return fail("hipMemcpy", e);
-    if ((e = hipMemcpy(c->d_py, py.data(), pb, hipMemcpyHostToDevice)) != hipSuccess) return fail("hipMemcpy", e);
+    if ((e = hipMalloc(&c->d_gx, nx * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc(&c->d_gy, ny * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMemcpy(c->d_gx, gx.data(), nx * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail("hipMemcpy", e);
+    if ((e = hipMemcpy(c->d_gy, gy.data(), ny * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+        return fail("hipMemcpy", e);
     if (!kc.empty()) {
         if ((e = hipMalloc(&c->d_kc, kc.size() * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
         if ((e = hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
@@ -167,7 +180,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (!c) return PDEVAL_ERR_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_px, (void*)c->d_py, (void*)c->d_kc, (void*)c->d_defer, (void*)c->d_cplx,
+    for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc, (void*)c->d_defer, (void*)c->d_defer2, (void*)c->d_cplx,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) hipFree(p);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -275,15 +288,22 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
 // ---------------------------------------------------------------------------- launches
 static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (n <= c->cap) return PDEVAL_OK;
-    if (c->d_defer) hipFree(c->d_defer);
-    if (c->d_cplx) hipFree(c->d_cplx);
-    c->d_defer = c->d_cplx = nullptr;
+    for (int64_t** p : {&c->d_defer, &c->d_defer2, &c->d_cplx}) {
+        if (*p) (void)hipFree(*p);
+        *p = nullptr;
+    }
     c->cap = 0;
     const int64_t cap = n < 1024 ? 1024 : n;
     HIPCHK(c, hipMalloc(&c->d_defer, cap * sizeof(int64_t)));
+    HIPCHK(c, hipMalloc(&c->d_defer2, cap * sizeof(int64_t)));
     HIPCHK(c, hipMalloc(&c->d_cplx, cap * sizeof(int64_t)));
     c->cap = cap;
     return PDEVAL_OK;
+}
+
+// dynamic LDS of one block: waves x (MAXD-1) stack slots x jet x 64 lanes (<= 160 KiB/CU)
+template <class T, int K, int MAXD> constexpr size_t stack_lds(int waves) {
+    return (size_t)waves * (MAXD - 1) * ((K + 1) * (K + 2) / 2) * 64 * sizeof(T);
 }
 
 template <int PROB>
@@ -294,8 +314,14 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.offsets = d_off;
     a.n_words = n_words;
     a.n = n;
-    a.px = c->d_px;
-    a.py = c->d_py;
+    for (int k = 0; k < 4; ++k) {
+        a.ref_x[k] = c->ref_x[k];
+        a.ref_y[k] = c->ref_y[k];
+    }
+    a.gx = c->d_gx;
+    a.gy = c->d_gy;
+    a.nx = c->nx;
+    a.ny = c->ny;
     a.kc = c->d_kc;
     a.n_ref = c->n_ref;
     a.n_pts = c->n_pts;
@@ -314,27 +340,41 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // candidate; deeper programs are appended to a device list
     a.defer_list = c->d_defer;
     a.defer_count = c->d_counts + 0;
-    hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256),
+                       (stack_lds<double, K, 2>(4)), s, a);
     HIPCHK(c, hipGetLastError());
-    // pass 2: the deferred programs, persistent over the device list (stack <= 8)
+    // pass 2: deferred programs with stack 3..4 (register stack), persistent over list 1;
+    // deeper ones go on to list 2
     KernelArgs b = a;
     b.list = c->d_defer;
     b.list_count = c->d_counts + 0;
-    b.defer_list = nullptr;  // depth <= PDEVAL_MAX_STACK is guaranteed by the flattener
-    const int64_t pblocks = std::min<int64_t>(blocks, 1024);
-    hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>), dim3((unsigned)pblocks),
-                       dim3(256), 0, s, b);
+    b.defer_list = c->d_defer2;
+    b.defer_count = c->d_counts + 2;
+    const int64_t pblocks = std::min<int64_t>(blocks, 2048);
+    // follow-up passes: one wave per block (their LDS stacks are deeper)
+    hipLaunchKernelGGL((validate_kernel<PROB, double, 4, true>), dim3((unsigned)(4 * pblocks)), dim3(64),
+                       (stack_lds<double, K, 4>(1)), s, b);
+    HIPCHK(c, hipGetLastError());
+    // pass 3: stack 5..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
+    KernelArgs b2 = a;
+    b2.list = c->d_defer2;
+    b2.list_count = c->d_counts + 2;
+    b2.defer_list = nullptr;
+    hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
+                       dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
+                       (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, b2);
     HIPCHK(c, hipGetLastError());
     if (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-        // pass 3: candidates not real at the reference point, in complex arithmetic
+        // pass 4: candidates not real at the reference point, in complex arithmetic
         KernelArgs x = a;
         x.list = c->d_cplx;
         x.list_count = c->d_counts + 1;
         x.cplx_list = nullptr;
         x.defer_list = nullptr;
-        const int64_t cblocks = std::min<int64_t>(blocks, 256);
-        hipLaunchKernelGGL((validate_kernel<PROB, cplx, 4, true>), dim3((unsigned)cblocks),
-                           dim3(256), 0, s, x);
+        const int64_t cblocks = std::min<int64_t>(blocks, 2048);
+        hipLaunchKernelGGL((validate_kernel<PROB, cplx, 4, true>), dim3((unsigned)(4 * cblocks)),
+                           dim3(64), (stack_lds<cplx, K, 4>(1)), s, x);
         HIPCHK(c, hipGetLastError());
     }
     return PDEVAL_OK;

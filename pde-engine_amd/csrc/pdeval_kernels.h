@@ -28,11 +28,15 @@ struct KernelArgs {
     const int64_t* list;        // optional: wave -> candidate index (NULL = identity)
     const int32_t* list_count;  // optional device count for list (persistent passes)
     int64_t list_cap;
-    const double* px;           // point coordinates, reference points first
-    const double* py;
+    // sample points: chunk 0 holds the reference points (lanes < n_ref), chunk c >= 1 the grid
+    // row x = gx[(c-1) / (ny/64)] (one x per chunk: a scalar), y = gy[.. + lane]
+    double ref_x[4], ref_y[4];
+    const double* gx;           // nx grid abscissae
+    const double* gy;           // ny grid ordinates (ny % 64 == 0)
+    int nx, ny;
     const double* kc;           // Kerr: 4 operator coefficients per point (NULL for FF)
     int n_ref;
-    int n_pts;
+    int n_pts;                  // n_ref + nx * ny
     int fp_pts[PDEVAL_FP_N];    // point indices whose u value is the fingerprint
     pdeval_params prm;
     pdeval_outputs out;
@@ -57,14 +61,23 @@ template <class T> struct Real;
 template <> struct Real<double> { static constexpr bool cplx_pass = false; };
 template <> struct Real<cplx> { static constexpr bool cplx_pass = true; };
 
+// Program words are wave-uniform: read them through the constant address space so they
+// become scalar loads (s_load_dword, served by the scalar cache) instead of vector loads +
+// readfirstlane -- one such dependent load per opcode per chunk was a large share of the
+// interpreter's time.
+typedef const __attribute__((address_space(4))) uint32_t* cword_ptr;
 __device__ __forceinline__ uint32_t rd_word(const int32_t* p) {
-    return (uint32_t)__builtin_amdgcn_readfirstlane(*p);
+    return *(cword_ptr)(p);
 }
 __device__ __forceinline__ double rd_imm(const int32_t* p) {
     // the two words following an opcode hold the f64 immediate, low word first
-    uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane(p[0]);
-    uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(p[1]);
+    const uint32_t lo = *(cword_ptr)(p);
+    const uint32_t hi = *(cword_ptr)(p + 1);
     return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ bool op_has_imm(uint32_t op) {
+    return op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC ||
+           op == PDOP_POW;
 }
 
 template <class T, int K> struct JetOps {
@@ -92,20 +105,54 @@ template <class T, int K> struct JetOps {
 #pragma unroll
         for (int i = 0; i < NC; ++i) t.c[i] = t.c[i] - a.c[i];
     }
+    // t = a * t in place: outputs in decreasing total degree; c_ij reads t_kl only for
+    // (k,l) <= (i,j), and no other output of degree i+j reads t_ij, so overwriting is safe
+    // (saves a jet of registers against a separate result)
     static PD_HD void mul(const J& a, J& t) {
-        J r;
-        jmul<T, K, K, K>(a.c, t.c, r.c);
-        t = r;
+#pragma unroll
+        for (int d = K; d >= 0; --d) {
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                const int i = d - j;
+                T s = a.c[0] * t.c[ji(i, j)];
+#pragma unroll
+                for (int d1 = 1; d1 <= d; ++d1)
+#pragma unroll
+                    for (int j1 = 0; j1 <= d1; ++j1) {
+                        const int i1 = d1 - j1, i2 = i - i1, j2 = j - j1;
+                        if (i2 < 0 || j2 < 0) continue;
+                        s = fmac(a.c[ji(i1, j1)], t.c[ji(i2, j2)], s);
+                    }
+                t.c[ji(i, j)] = s;
+            }
+        }
     }
     static PD_HD void div(const J& a, J& t) {  // t = a / t
         J r;
         jdiv<T, K>(a.c, t.c, r.c);
         t = r;
     }
-    static PD_HD void rdiv(const J& a, J& t) {  // t = t / a
-        J r;
-        jdiv<T, K>(t.c, a.c, r.c);
-        t = r;
+    // t = t / a in place: outputs in increasing degree; c_dj needs t_dj (read before it is
+    // overwritten) and outputs of lower degree (already in t)
+    static PD_HD void rdiv(const J& a, J& t) {
+        const T inv = recip(a.c[0]);
+#pragma unroll
+        for (int d = 0; d <= K; ++d) {
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                const int i = d - j;
+                T s = t.c[ji(i, j)];
+#pragma unroll
+                for (int d1 = 1; d1 <= d; ++d1)
+#pragma unroll
+                    for (int j1 = 0; j1 <= d1; ++j1) {
+                        const int i1 = d1 - j1, i2 = i - i1, j2 = j - j1;
+                        if (i2 < 0 || j2 < 0) continue;
+                        s = fmac(-a.c[ji(i1, j1)], t.c[ji(i2, j2)], s);
+                    }
+                t.c[ji(i, j)] = qdiv(s, a.c[0], inv);
+            }
+        }
     }
     static PD_HD void scale(J& t, T s) {
 #pragma unroll
@@ -147,28 +194,53 @@ template <class T, int K> struct JetOps {
         set_const(a, c);
         div(a, t);
     }
-    static PD_HD void pown(J& t, int n) {  // n >= 2
-        J base = t, r;
-        bool have = false;
-        while (n > 0) {
-            if (n & 1) {
-                if (have) {
-                    J tmp;
-                    jmul<T, K, K, K>(r.c, base.c, tmp.c);
-                    r = tmp;
-                } else {
-                    r = base;
-                    have = true;
+    // t = t*t with the symmetric half of the products
+    static PD_HD void square(J& t) {
+        J r;
+#pragma unroll
+        for (int d = K; d >= 0; --d) {
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                T s = zero<T>();
+                bool first = true;
+                // pairs (k, d-k) of degrees with k <= d-k; the (i1,j1) x (i2,j2) terms with
+                // (i1,j1) < (i2,j2) lexicographically are doubled
+#pragma unroll
+                for (int d1 = 0; d1 <= d; ++d1) {
+#pragma unroll
+                    for (int j1 = 0; j1 <= d1; ++j1) {
+                        const int i1 = d1 - j1, i = d - j, i2 = i - i1, j2 = j - j1;
+                        if (i2 < 0 || j2 < 0) continue;
+                        const int k1 = ji(i1, j1), k2 = ji(i2, j2);
+                        if (k1 > k2) continue;
+                        const T prod = (k1 == k2) ? t.c[k1] * t.c[k2] : (t.c[k1] + t.c[k1]) * t.c[k2];
+                        s = first ? prod : s + prod;
+                        first = false;
+                    }
                 }
-            }
-            n >>= 1;
-            if (n) {
-                J sq;
-                jmul<T, K, K, K>(base.c, base.c, sq.c);
-                base = sq;
+                r.c[ji(d - j, j)] = s;
             }
         }
         t = r;
+    }
+    static PD_HD void pown(J& t, int n) {  // 2 <= n <= 16
+        if (n == 2) {
+            square(t);
+            return;
+        }
+        J base = t;
+        if (n == 3) {
+            square(t);
+            mul(base, t);
+            return;
+        }
+        if (n == 4) {
+            square(t);
+            square(t);
+            return;
+        }
+        // general: t = base^n by repeated multiplication (rare exponents)
+        for (int k = 1; k < n; ++k) mul(base, t);
     }
     static PD_HD void powa(J& t, double alpha) {
         T f[K + 1];
@@ -228,73 +300,100 @@ struct PointResult {
 // MAG = true evaluates the same expression on magnitudes with every difference turned into
 // a sum: S >= sum of |monomials| of the fully expanded determinant.
 template <class T, bool MAG> struct FFEpi {
+    // Everything is read straight from u's Taylor coefficients (no materialized copies of
+    // p = u_rho, q = u_z), and each intermediate dies as soon as its Lie derivative is
+    // formed: this keeps the epilogue's live set small enough for more waves per SIMD.
     static PD_HD T sgn(T a) { return MAG ? a : -a; }
-    static PD_HD T eval(const T* u, double rho) {
-        T p[10], q[10];
-#pragma unroll
-        for (int d = 0; d <= 3; ++d)
-#pragma unroll
-            for (int j = 0; j <= d; ++j) {
-                const int i = d - j;
-                p[ji(i, j)] = u[ji(i + 1, j)] * (double)(i + 1);
-                q[ji(i, j)] = u[ji(i, j + 1)] * (double)(j + 1);
-            }
-        // 1/rho jet (rho direction only): (-1)^i / rho^(i+1)
-        const double r0 = 1.0 / rho;
-        const double ri[3] = {r0, (MAG ? 1.0 : -1.0) * r0 * r0, r0 * r0 * r0};
-        T A[6], B[6];
-#pragma unroll
-        for (int d = 0; d <= 2; ++d)
-#pragma unroll
-            for (int j = 0; j <= d; ++j) {
-                const int i = d - j;
-                T s = p[ji(i + 1, j)] * (double)(i + 1) + q[ji(i, j + 1)] * (double)(j + 1);
-                T pr = p[ji(i, j)] * ri[0];
-#pragma unroll
-                for (int i1 = 1; i1 <= i; ++i1) pr = fmac(p[ji(i - i1, j)], from_real<T>(ri[i1]), pr);
-                A[ji(i, j)] = s + sgn(pr);
-            }
-        {
-            T pp[6], qq[6];
-            jmul<T, 3, 3, 2>(p, p, pp);
-            jmul<T, 3, 3, 2>(q, q, qq);
-#pragma unroll
-            for (int i = 0; i < 6; ++i) B[i] = pp[i] + qq[i];
-        }
-        // L_T f = q f_rho - p f_z, order 1 from order-2 f
-        T LA[3], LB[3];
-        lie1(p, q, A, LA);
-        lie1(p, q, B, LB);
-        // order 0 from order 1
-        const T L2A = q[0] * LA[ji(1, 0)] + sgn(p[0] * LA[ji(0, 1)]);
-        const T L2B = q[0] * LB[ji(1, 0)] + sgn(p[0] * LB[ji(0, 1)]);
-        return LA[0] * L2B + sgn(LB[0] * L2A);
+    // MAG: read |c_ij| (a free source modifier on the VALU), so no copy of u is made
+    static PD_HD T rd(const T* u, int k) {
+        if constexpr (MAG) return fabs(u[k]);
+        else return u[k];
     }
-    static PD_HD void lie1(const T* p, const T* q, const T* f, T* out) {
-        T fr[3], fz[3];
+    static PD_HD T U(const T* u, int i, int j) { return rd(u, ji(i, j)); }
+    // p_ij = (i+1) c_{i+1,j},  q_ij = (j+1) c_{i,j+1}
+    static PD_HD T P(const T* u, int i, int j) { return rd(u, ji(i + 1, j)) * (double)(i + 1); }
+    static PD_HD T Q(const T* u, int i, int j) { return rd(u, ji(i, j + 1)) * (double)(j + 1); }
+
+    // L_T f (order 1) = q f_rho - p f_z for f of order 2
+    static PD_HD void lie1(const T* u, const T* f, T* out) {
+        const T p00 = P(u, 0, 0), p10 = P(u, 1, 0), p01 = P(u, 0, 1);
+        const T q00 = Q(u, 0, 0), q10 = Q(u, 1, 0), q01 = Q(u, 0, 1);
+        // f is an intermediate (already a magnitude in the MAG evaluation)
+        const T fr00 = f[ji(1, 0)], fr10 = f[ji(2, 0)] * 2.0, fr01 = f[ji(1, 1)];
+        const T fz00 = f[ji(0, 1)], fz10 = f[ji(1, 1)], fz01 = f[ji(0, 2)] * 2.0;
+        out[0] = q00 * fr00 + sgn(p00 * fz00);
+        out[ji(1, 0)] = fmac(q00, fr10, q10 * fr00) + sgn(fmac(p00, fz10, p10 * fz00));
+        out[ji(0, 1)] = fmac(q00, fr01, q01 * fr00) + sgn(fmac(p00, fz01, p01 * fz00));
+    }
+
+    static PD_HD T eval(const T* u, double rho) {
+        const double r0 = 1.0 / rho;
+        // 1/rho jet in the rho direction: (-1)^i / rho^(i+1)
+        const double ri[3] = {r0, (MAG ? 1.0 : -1.0) * r0 * r0, r0 * r0 * r0};
+        T LA[3], LB[3];
+        {
+            // A = p_rho + q_z - p / rho   (validator.py:323), order 2
+            T A[6];
 #pragma unroll
-        for (int d = 0; d <= 1; ++d)
+            for (int d = 0; d <= 2; ++d)
 #pragma unroll
-            for (int j = 0; j <= d; ++j) {
-                const int i = d - j;
-                fr[ji(i, j)] = f[ji(i + 1, j)] * (double)(i + 1);
-                fz[ji(i, j)] = f[ji(i, j + 1)] * (double)(j + 1);
-            }
-        T a[3], b[3];
-        jmul<T, 1, 1, 1>(q, fr, a);
-        jmul<T, 1, 1, 1>(p, fz, b);
+                for (int j = 0; j <= d; ++j) {
+                    const int i = d - j;
+                    T s = U(u, i + 2, j) * (double)((i + 1) * (i + 2));
+                    s = fmac(U(u, i, j + 2), from_real<T>((double)((j + 1) * (j + 2))), s);
+                    T pr = P(u, i, j) * ri[0];
 #pragma unroll
-        for (int i = 0; i < 3; ++i) out[i] = a[i] + sgn(b[i]);
+                    for (int i1 = 1; i1 <= i; ++i1) pr = fmac(P(u, i - i1, j), from_real<T>(ri[i1]), pr);
+                    A[ji(i, j)] = s + sgn(pr);
+                }
+            lie1(u, A, LA);
+        }
+        {
+            // B = p^2 + q^2   (validator.py:324), order 2
+            T B[6];
+#pragma unroll
+            for (int d = 0; d <= 2; ++d)
+#pragma unroll
+                for (int j = 0; j <= d; ++j) {
+                    const int i = d - j;
+                    T s = zero<T>();
+#pragma unroll
+                    for (int d1 = 0; d1 <= d; ++d1)
+#pragma unroll
+                        for (int j1 = 0; j1 <= d1; ++j1) {
+                            const int i1 = d1 - j1, i2 = i - i1, j2 = j - j1;
+                            if (i2 < 0 || j2 < 0) continue;
+                            s = fmac(P(u, i1, j1), P(u, i2, j2), s);
+                            s = fmac(Q(u, i1, j1), Q(u, i2, j2), s);
+                        }
+                    B[ji(i, j)] = s;
+                }
+            lie1(u, B, LB);
+        }
+        // L_T^2 f (order 0) = q (L_T f)_rho - p (L_T f)_z
+        const T p00 = P(u, 0, 0), q00 = Q(u, 0, 0);
+        const T L2A = q00 * LA[ji(1, 0)] + sgn(p00 * LA[ji(0, 1)]);
+        const T L2B = q00 * LB[ji(1, 0)] + sgn(p00 * LB[ji(0, 1)]);
+        // det[[L_T A, L_T B], [L_T^2 A, L_T^2 B]]   (validator.py:347)
+        return LA[0] * L2B + sgn(LB[0] * L2A);
     }
 };
 
 template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u, double rho) {
     PointResult r;
     const T det = FFEpi<T, false>::eval(u, rho);
-    double m[15];
+    // keep the signed and the magnitude evaluations apart: interleaved, the scheduler keeps
+    // both sets of intermediates live
+    __builtin_amdgcn_sched_barrier(0);
+    double S;
+    if constexpr (Real<T>::cplx_pass) {
+        double m[15];
 #pragma unroll
-    for (int i = 0; i < 15; ++i) m[i] = mag(u[i]);
-    const double S = FFEpi<double, true>::eval(m, rho);
+        for (int i = 0; i < 15; ++i) m[i] = mag(u[i]);
+        S = FFEpi<double, true>::eval(m, rho);
+    } else {
+        S = FFEpi<double, true>::eval(u, rho);
+    }
     r.res_abs = mag(det);
     if constexpr (Real<T>::cplx_pass) {
         r.res_re = ((const cplx*)&det)->re;
@@ -392,27 +491,48 @@ template <class T, int K, int MAXD> struct Interp {
         }
     }
 
+    // Operand stack below the top-of-stack jet: kept in LDS, not VGPRs, so the registers
+    // hold one jet (the accumulator) plus the op's temporaries -- more waves per SIMD.
+    // Layout per wave: [slot][coefficient][lane] -> each lane touches only its own doubles and
+    // consecutive lanes hit consecutive 8-byte words (no bank conflicts, no barriers needed).
+    static constexpr int NCJ = nc(K);
+    static __device__ __forceinline__ void lds_store(T* base, int slot, int lane, const J& t) {
+#pragma unroll
+        for (int c = 0; c < NCJ; ++c) base[(slot * NCJ + c) * 64 + lane] = t.c[c];
+    }
+    static __device__ __forceinline__ void lds_load(const T* base, int slot, int lane, J& t) {
+#pragma unroll
+        for (int c = 0; c < NCJ; ++c) t.c[c] = base[(slot * NCJ + c) * 64 + lane];
+    }
+
     // Evaluate program words [pc, end) at point (x, y); result jet in T.
-    static __device__ __forceinline__ int run(const int32_t* ops, int64_t pc, int64_t end, double x, double y, J& acc) {
-        J S[MAXD - 1];
+    static __device__ __forceinline__ int run(const int32_t* ops, int64_t pc, int64_t end, double x, double y,
+                                              J& acc, T* stk, int lane) {
         int d = 0;
-        while (pc < end) {
-            const uint32_t w = rd_word(ops + pc);
+        if (pc >= end) return RUN_BAD;
+        uint32_t w = rd_word(ops + pc);
+        for (;;) {
             const uint32_t op = w & 0xffu;
-            ++pc;
+            // immediate and next opcode word are fetched before this op's jet arithmetic, so
+            // their scalar-load latency hides under it
+            double imm = 0.0;
+            int64_t npc = pc + 1;
+            if (op_has_imm(op)) {
+                if (pc + 3 > end) return RUN_BAD;
+                imm = rd_imm(ops + pc + 1);
+                npc = pc + 3;
+            }
+            const uint32_t wn = (npc < end) ? rd_word(ops + npc) : 0u;
             switch (op) {
                 case PDOP_PUSH_X:
                 case PDOP_PUSH_Y:
                 case PDOP_PUSH_C:
                 case PDOP_PUSH_I: {
-                    if (d >= MAXD) return RUN_BAD;
-                    if (d > 0) push_down<0>(S, d, acc);
+                    if (d > 0 && d < MAXD) lds_store(stk, d - 1, lane, acc);
                     if (op == PDOP_PUSH_X) O::set_var(acc, x, 0);
                     else if (op == PDOP_PUSH_Y) O::set_var(acc, y, 1);
                     else if (op == PDOP_PUSH_C) {
-                        if (pc + 2 > end) return RUN_BAD;
-                        O::set_const(acc, from_real<T>(rd_imm(ops + pc)));
-                        pc += 2;
+                        O::set_const(acc, from_real<T>(imm));
                     } else {
                         if constexpr (Real<T>::cplx_pass) O::set_const(acc, cplx{0.0, 1.0});
                         else return RUN_UNSUPPORTED;
@@ -422,26 +542,25 @@ template <class T, int K, int MAXD> struct Interp {
                 }
                 case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB:
                 case PDOP_MUL: case PDOP_DIV: case PDOP_RDIV: {
-                    if (d < 2) return RUN_BAD;
-                    below<0>(S, d, op, acc);
+                    if (d >= 2 && d <= MAXD) {
+                        J lhs;
+                        lds_load(stk, d - 2, lane, lhs);
+                        binop(op, lhs, acc);
+                    }
                     --d;
                     break;
                 }
                 case PDOP_ADDC: case PDOP_MULC: case PDOP_RDIVC: {
-                    if (d < 1 || pc + 2 > end) return RUN_BAD;
-                    const double c = rd_imm(ops + pc);
-                    pc += 2;
+                    const double c = imm;
                     if (op == PDOP_ADDC) acc.c[0] = acc.c[0] + from_real<T>(c);
                     else if (op == PDOP_MULC) O::scale(acc, from_real<T>(c));
                     else O::rdivc(acc, from_real<T>(c));
                     break;
                 }
                 case PDOP_NEG:
-                    if (d < 1) return RUN_BAD;
                     O::scale(acc, from_real<T>(-1.0));
                     break;
                 case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: {
-                    if (d < 1) return RUN_BAD;
                     const bool isx = (op == PDOP_ADD_X || op == PDOP_SUB_X);
                     const double sg = (op == PDOP_ADD_X || op == PDOP_ADD_Y) ? 1.0 : -1.0;
                     acc.c[0] = acc.c[0] + from_real<T>(sg * (isx ? x : y));
@@ -449,27 +568,26 @@ template <class T, int K, int MAXD> struct Interp {
                     acc.c[idx] = acc.c[idx] + from_real<T>(sg);
                     break;
                 }
-                case PDOP_MUL_X: if (d < 1) return RUN_BAD; O::mul_var(acc, x, 0); break;
-                case PDOP_MUL_Y: if (d < 1) return RUN_BAD; O::mul_var(acc, y, 1); break;
-                case PDOP_DIV_X: if (d < 1) return RUN_BAD; O::div_var(acc, x, 0); break;
-                case PDOP_DIV_Y: if (d < 1) return RUN_BAD; O::div_var(acc, y, 1); break;
+                case PDOP_MUL_X: O::mul_var(acc, x, 0); break;
+                case PDOP_MUL_Y: O::mul_var(acc, y, 1); break;
+                case PDOP_DIV_X: O::div_var(acc, x, 0); break;
+                case PDOP_DIV_Y: O::div_var(acc, y, 1); break;
                 case PDOP_POWN:
-                    if (d < 1) return RUN_BAD;
                     O::pown(acc, (int)((w >> 8) & 0xffu));
                     break;
                 case PDOP_POW: {
-                    if (d < 1 || pc + 2 > end) return RUN_BAD;
-                    const double a = rd_imm(ops + pc);
-                    pc += 2;
-                    O::powa(acc, a);
+                    O::powa(acc, imm);
                     break;
                 }
-                case PDOP_SQRT: if (d < 1) return RUN_BAD; O::sqrtj(acc); break;
-                case PDOP_EXP: if (d < 1) return RUN_BAD; O::expj(acc); break;
-                case PDOP_LOG: if (d < 1) return RUN_BAD; O::logj(acc); break;
-                case PDOP_ABS: if (d < 1) return RUN_BAD; absj<K>(acc); break;
+                case PDOP_SQRT: O::sqrtj(acc); break;
+                case PDOP_EXP: O::expj(acc); break;
+                case PDOP_LOG: O::logj(acc); break;
+                case PDOP_ABS: absj<K>(acc); break;
                 default: return RUN_UNSUPPORTED;
             }
+            if (npc >= end) break;
+            pc = npc;
+            w = wn;
         }
         return d == 1 ? RUN_OK : RUN_BAD;
     }
@@ -478,12 +596,17 @@ template <class T, int K, int MAXD> struct Interp {
 // ------------------------------------------------------------------ the kernel
 // PROB: PDEVAL_PROBLEM_FORCE_FREE (K = 4) or PDEVAL_PROBLEM_KERR (K = 2).
 template <int PROB, class T, int MAXD, bool PERSISTENT>
-__global__ __launch_bounds__(256, 2) void validate_kernel(KernelArgs a) {
+#ifndef PD_WAVES_PER_SIMD
+#define PD_WAVES_PER_SIMD 4
+#endif
+__global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
     using I = Interp<T, K, MAXD>;
     using J = typename I::J;
     const int lane = threadIdx.x & 63;
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+    T* stk = reinterpret_cast<T*>(pd_lds) + (size_t)wib * (MAXD - 1) * nc(K) * 64;
     const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
     // persistent variants stride over a device work list; the first pass is one wave per
     // candidate (a single iteration)
@@ -527,14 +650,30 @@ __global__ __launch_bounds__(256, 2) void validate_kernel(KernelArgs a) {
         double qmax = 0.0;
         int nbad = 0, nnonfin = 0, nfin = 0;
         bool grad_nz = false;
-        const int nchunks = (a.n_pts + 63) >> 6;
+        // chunk 0: the reference points; chunks 1..: one 64-point slice of a grid row each
+        const int per_row = a.ny >> 6;
+        const int nchunks = 1 + a.nx * per_row;
+        const double y_lane = a.gy[lane];  // row slice 0; other slices reload below
         for (int ch = 0; ch < nchunks && status < 0; ++ch) {
-            const int p = ch * 64 + lane;
-            const bool active = p < a.n_pts;
-            const int pp = active ? p : 0;
-            const double x = a.px[pp], y = a.py[pp];
+            bool active;
+            int p;               // point index: reference points first, then the grid row-major
+            double x, y;
+            if (ch == 0) {
+                active = lane < a.n_ref;
+                p = lane;
+                const int l = active ? lane : 0;
+                x = l == 0 ? a.ref_x[0] : (l == 1 ? a.ref_x[1] : (l == 2 ? a.ref_x[2] : a.ref_x[3]));
+                y = l == 0 ? a.ref_y[0] : (l == 1 ? a.ref_y[1] : (l == 2 ? a.ref_y[2] : a.ref_y[3]));
+            } else {
+                const int row = (ch - 1) / per_row, sl = (ch - 1) - row * per_row;
+                active = true;
+                p = a.n_ref + row * a.ny + sl * 64 + lane;
+                x = *(const __attribute__((address_space(4))) double*)(a.gx + row);   // scalar
+                y = per_row == 1 ? y_lane : a.gy[sl * 64 + lane];
+            }
+            const int pp = p;
             J u;
-            const int rc = I::run(a.ops, beg + 1, end, x, y, u);
+            const int rc = I::run(a.ops, beg + 1, end, x, y, u, stk, lane);
             if (rc == RUN_UNSUPPORTED) { status = PDEVAL_CLS_UNSUPPORTED; break; }
             if (rc == RUN_BAD) { status = PDEVAL_CLS_BAD_PROGRAM; break; }
             PointResult r;
