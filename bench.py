@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
-"""Benchmark: validated candidates/s of the MI355X validator on the force-free depth-4 batch.
+"""Benchmark: validated candidates/s of the MI355X validator on the force-free depth-4 batch,
+and the wall time to recover the 7 force-free paper solutions at depth 4.
 
-Workload (BASELINE.json configs[2], "force_free --max-depth 4 on 1xMI355X"; SURVEY.md §8d C3/C4):
-the candidates of the reference's depth-4 force-free stream (tests/golden/streams, compiled
-into data/force_free_d4_*.npz), tiled and shuffled with seed 0 into a batch of --n candidates
-per GPU.  One "step" = one validation pass of the whole batch: every candidate's program is
-evaluated in jets at the reference point and on the 64x64 (rho, z) grid (4097 points), the
-foliation determinant and its scaled zero test are applied and the verdict bitmap + per-
-candidate outputs are written to HBM.  Inputs are resident in HBM before timing starts.
+Workload (BASELINE.json configs[2], "force_free --max-depth 4 on 1xMI355X"; SURVEY.md §8d C3):
+the 142,004 candidates of the reference's depth-4 force-free stream that pass its pre-validate
+filters (tests/golden/streams/force_free_d4_validated.txt.gz, compiled once into
+data/force_free_d4_validated.npz), tiled and shuffled with seed 0 into --n candidates per GPU.
+One "step" = one validation pass of the whole batch: every candidate's program is evaluated
+in jets at the reference point and on the 64x64 (rho, z) grid (4097 points), the foliation
+determinant and its scaled zero test are applied and the verdict bitmap + per-candidate
+outputs are written to HBM.  Inputs are resident in HBM before timing starts.
 
-Multi-GPU (torchrun, one process per GPU): each rank validates its own contiguous shard
-(weak scaling, no data-path collective); after timing, one RCCL all-gather of the verdict
-bitmaps assembles the global result on every rank.
+Multi-GPU (torchrun, one process per GPU): the global batch (--n per rank) is cut into
+contiguous shards (pdeval.shard); every rank validates its own shard (weak scaling, no
+data-path collective); after timing, one RCCL all-gather of the verdict bitmaps assembles the
+global result on every rank.
 """
 import argparse
 import ctypes as C
+import glob
 import json
 import os
 import sys
@@ -28,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, 'tests'))
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (spec; MI355X_MICROARCH.md lists FP32 157.3 = 2x)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s"
+DOMINANT = 'validate_kernel<0, double, 2, false>'
 
 
 def load_workload(problem):
@@ -35,7 +40,7 @@ def load_workload(problem):
         p = os.path.join(ROOT, 'data', name)
         if os.path.exists(p):
             z = np.load(p, allow_pickle=False)
-            return name, z['ops'], z['offsets']
+            return name, z['ops'], z['offsets'], z['exprs']
     raise FileNotFoundError('data/*_d4_*.npz missing')
 
 
@@ -49,6 +54,21 @@ def gather_programs(ops, offsets, idx):
     return ops[starts + within], new_off
 
 
+def pmc_traffic(n_per_launch):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
+    (profiles/*_pmc.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc
+    passes), scaled to this launch's candidate count; None if there is none."""
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        s = json.load(f)
+    k = s.get('kernels', {}).get(DOMINANT)
+    if not k or not k.get('candidates'):
+        return None, os.path.basename(files[-1])
+    return k['hbm_bytes_per_launch'] / k['candidates'] * n_per_launch, os.path.basename(files[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -57,15 +77,18 @@ def main():
     ap.add_argument('--n', type=int, default=1 << 20, help='candidates per GPU per step')
     ap.add_argument('--problem', default='force_free')
     ap.add_argument('--early-exit', action='store_true',
-                    help='stop after the point stage for point-rejects (the reference\'s control flow)')
+                    help='headline run stops after the point stage for point-rejects')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='CPU-baseline time budget')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--no-extras', action='store_true',
+                    help='skip the early-exit / host-buffer / time-to-solutions legs')
     a = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     from pdeval import _lib
     from pdeval.opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR, FP_N
+    from pdeval.shard import gather_verdicts, shard_ranges
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -76,16 +99,19 @@ def main():
     dev = torch.device(f'cuda:{local}')
     pid = PROBLEM_FORCE_FREE if a.problem == 'force_free' else PROBLEM_KERR
 
-    wname, ops_all, off_all = load_workload(a.problem)
+    wname, ops_all, off_all, exprs_all = load_workload(a.problem)
     nprog = len(off_all) - 1
     total = a.n * world
     rng = np.random.default_rng(0)
     tiled = np.tile(np.arange(nprog, dtype=np.int64), (total + nprog - 1) // nprog)[:total]
     rng.shuffle(tiled)
-    idx = tiled[rank * a.n:(rank + 1) * a.n]
+    ranges = shard_ranges(total, world)
+    s0, s1 = ranges[rank]
+    idx = tiled[s0:s1]
+    n = len(idx)
     ops, off = gather_programs(ops_all, off_all, idx)
 
-    # algorithmic work of the batch (DESIGN.md "Roofline")
+    # algorithmic work of the batch
     lib = _lib.load()
     flops_prog = np.array([lib.pdeval_program_flops(pid, ops_all[off_all[i]:].ctypes.data,
                                                     int(off_all[i + 1] - off_all[i]))
@@ -94,11 +120,10 @@ def main():
     npts, nref = ctx.n_points, ctx.n_ref
     flops_step = float(flops_prog[idx].sum()) * npts
     out_bytes_per = 1 + 8 + 8 * nref + 8 + 4 + 4 + 8 * FP_N + 1.0 / 8
-    bytes_step = ops.nbytes + off.nbytes + a.n * out_bytes_per
+    bytes_step = ops.nbytes + off.nbytes + n * out_bytes_per
 
     d_ops = torch.from_numpy(ops).to(dev)
     d_off = torch.from_numpy(off).to(dev)
-    n = a.n
     outs = dict(verdict_bits=torch.zeros(((n + 31) // 32) * 4, dtype=torch.uint8, device=dev),
                 status=torch.zeros(n, dtype=torch.uint8, device=dev),
                 q_ref=torch.zeros(n, dtype=torch.float64, device=dev),
@@ -115,69 +140,108 @@ def main():
     torch.cuda.synchronize(dev)
     stream = torch.cuda.Stream(dev)
 
-    def step():
+    def step(p):
         ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out,
-                            params=prm, stream=stream.cuda_stream, zero_bits=True)
+                            params=p, stream=stream.cuda_stream, zero_bits=True)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(a.steps)]
-    t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
-        step()
-        e.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    def timed(p, steps, warmup):
+        for _ in range(warmup):
+            step(p)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        t0 = time.perf_counter()
+        for s, e in ev:
+            s.record(stream)
+            step(p)
+            e.record(stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        kern = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), kern
+
+    elapsed, kern_ms = timed(prm, a.steps, a.warmup)
 
     # the one exchange step: all-gather of the verdict bitmaps over RCCL
-    bits = outs['verdict_bits']
     if world > 1:
-        allbits = torch.empty(world * bits.numel(), dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(allbits, bits)
+        verdict_all = gather_verdicts(outs['verdict_bits'], ranges)
     else:
-        allbits = bits
+        verdict_all = np.unpackbits(outs['verdict_bits'].cpu().numpy(), bitorder='little')[:n].astype(bool)
     status = outs['status'].cpu().numpy()
-    n_acc_local = int(np.unpackbits(bits.cpu().numpy(), bitorder='little')[:n].sum())
 
+    # size-independent checks at full size: duplicates of one program (the batch is tiled)
+    # get one class, and the streamable paper solutions are accepted wherever they occur
+    first = np.full(nprog, 255, dtype=np.int16)
+    first[idx[::-1]] = status[::-1]
+    consistent = bool(np.array_equal(first[idx], status))
+
+    res = None
     if rank == 0:
         value = total * a.steps / elapsed
         achieved_tf = flops_step / (kern_ms * 1e-3) / 1e12
         achieved_gbs = bytes_step / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(n)
         res = {
             'metric': 'validated candidates/sec (force-free depth-4 batch, 64x64 grid + p*)',
             'value': value, 'unit': 'candidates/s', 'n_gpus': world, 'steps': a.steps,
             'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': f'{a.problem} depth-4 candidates ({wname}, {nprog} programs) '
-                                   f'tiled+shuffled(seed 0) to {a.n}/GPU; 64x64 grid + ref point',
+            'config': {'workload': f'{a.problem} depth-4 validated candidates ({wname}, {nprog} '
+                                   f'programs) tiled+shuffled(seed 0) to {a.n}/GPU; 64x64 grid + ref point',
                        'problem': a.problem, 'candidates_per_gpu': a.n, 'points_per_candidate': npts,
                        'full_grid': not a.early_exit, 'parallelism': f'shard{world}'},
             'roofline': {'bound': 'valu_fp64', 'achieved': achieved_tf, 'peak': FP64_PEAK_TFLOPS,
-                         'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS, 'traffic': None,
+                         'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS,
+                         'traffic': traffic, 'traffic_source': traffic_src,
                          'kernel_ms': kern_ms, 'flops_per_step': flops_step},
             'roofline_hbm': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
                              'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
                              'bytes_per_step': bytes_step},
-            'accepted_local': n_acc_local,
-            'status_hist': np.bincount(status, minlength=7).tolist(),
+            'accepted': int(verdict_all.sum()),
+            'status_hist': np.bincount(status, minlength=8).tolist(),
+            'duplicates_consistent': consistent,
         }
+
+    if not a.no_extras and world == 1:
+        # the reference's control flow: stop after the point stage for point-rejects (same
+        # verdicts; reported beside, never as, the headline value)
+        pe = _lib.default_params(pid)
+        pe.full_grid = 0
+        bits_full = outs['verdict_bits'].clone()
+        el_e, _ = timed(pe, a.steps, 1)
+        same = bool(torch.equal(bits_full, outs['verdict_bits']))
+        res['value_early_exit'] = total * a.steps / el_e
+        res['early_exit_verdicts_identical'] = same
+        # host buffers in and out (PCIe-inclusive), one synchronous C-ABI call
+        t0 = time.perf_counter()
+        ctx.validate(ops, off, prm)
+        res['value_host_buffers'] = n / (time.perf_counter() - t0)
+        # wall time to the 7 force-free paper solutions at depth 4 (BASELINE.json metric)
+        if pid == PROBLEM_FORCE_FREE:
+            from pdeval import problem_defs as P
+            from pdeval.discovery import find_known_solutions
+            t0 = time.perf_counter()
+            rec = find_known_solutions(ctx, P.force_free(), ops_all, off_all, exprs_all)
+            res['time_to_7_solutions_s'] = time.perf_counter() - t0
+            res['solutions_found'] = rec.n_found
+            res['solutions'] = {k: v for k, v in rec.found.items()}
+            res['solution_stream_hits'] = rec.stream_hits
+            res['time_to_7_breakdown_s'] = {k: round(v, 4) for k, v in rec.seconds.items()}
+
+    if rank == 0:
         if not a.no_cpu and world == 1:
             res['cpu_baseline'] = cpu_baseline(pid, ops_all, off_all, idx, a.cpu_seconds)
         print(json.dumps(res))
+    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -194,7 +258,7 @@ def cpu_baseline(pid, ops_all, off_all, idx, budget_s):
         done += 64
     dt = time.perf_counter() - t0
     return {'value': done / dt, 'unit': 'candidates/s', 'cores': 1, 'kind': 'port',
-            'sample': f'first {done} candidates of this batch (same 4097 points each), '
+            'sample': f'first {done} candidates of this batch (same 4097 points each, full grid), '
                       f'C oracle oracle/jet_oracle.c, 1 thread, {dt:.1f}s'}
 
 

@@ -43,8 +43,10 @@ def _is_leaf(n) -> bool:
     return n[0] in ('x', 'y', 'c')
 
 
-def _const(v) -> tuple:
-    return ('c', float(v))
+def _const(v, rational: bool = True) -> tuple:
+    # ('c', value) for a rational constant, ('c', value, False) for an irrational one (E, pi,
+    # a Float); only _det_kind looks at the third field
+    return ('c', float(v)) if rational else ('c', float(v), False)
 
 
 def _num_to_float(e: sp.Basic) -> float:
@@ -79,13 +81,13 @@ class _Lower:
         if e.is_Number:
             if not e.is_Rational:
                 self.irrational_const = True
-            return _const(_num_to_float(e))
+            return _const(_num_to_float(e), bool(e.is_Rational))
         if e is sp.E:
             self.irrational_const = True
-            return _const(math.e)
+            return _const(math.e, False)
         if e is sp.pi:
             self.irrational_const = True
-            return _const(math.pi)
+            return _const(math.pi, False)
         if e is sp.I:
             self.uses_i = True
             return ('i',)
@@ -106,11 +108,13 @@ class _Lower:
     def add(self, e: sp.Add):
         const = 0.0
         have_const = False
+        const_rational = True
         terms: List[Tuple[int, tuple]] = []
         for t in e.args:
             if t.is_Number and t.is_real:
                 const += _num_to_float(t)
                 have_const = True
+                const_rational = const_rational and bool(t.is_Rational)
                 continue
             sign = 1
             if t.is_Mul and t.args[0].is_Number and t.args[0].is_real and t.args[0] < 0:
@@ -119,7 +123,7 @@ class _Lower:
                 sign = -1
             terms.append((sign, self.node(t)))
         if not terms:
-            return _const(const)
+            return _const(const, const_rational)
         # positive terms first (so no leading negation is needed), heavy operands first
         terms.sort(key=lambda st: (st[0] < 0, -_need(st[1])))
         sign, acc = terms[0]
@@ -128,16 +132,18 @@ class _Lower:
         for sign, t in terms[1:]:
             acc = ('add' if sign > 0 else 'sub', acc, t)
         if have_const and const != 0.0:
-            acc = ('add', acc, _const(const))
+            acc = ('add', acc, _const(const, const_rational))
         return acc
 
     def mul(self, e: sp.Mul):
         coef = 1.0
+        coef_rational = True
         num: List[tuple] = []
         den: List[tuple] = []
         for f in e.args:
             if f.is_Number and f.is_real:
                 coef *= _num_to_float(f)
+                coef_rational = coef_rational and bool(f.is_Rational)
                 continue
             if f.is_Pow and f.exp.is_Integer and f.exp < 0:
                 n = -int(f.exp)
@@ -160,11 +166,11 @@ class _Lower:
             if coef == -1.0:
                 acc = ('neg', acc)
             elif coef != 1.0:
-                acc = ('mul', acc, _const(coef))
+                acc = ('mul', acc, _const(coef, coef_rational))
             return acc
         if den:
-            return ('div', _const(coef), product(den))
-        return _const(coef)
+            return ('div', _const(coef, coef_rational), product(den))
+        return _const(coef, coef_rational)
 
     def _pown(self, b, n: int):
         if n == 1:
@@ -335,6 +341,101 @@ def _op_positions(body: Sequence[int]):
         i += 3 if (body[i] & 0xff) in HAS_IMM else 1
 
 
+# --------------------------------------------------------------------------- det rationality
+def _frac(v: float) -> Fraction:
+    return Fraction(v).limit_denominator(1 << 12)
+
+
+def _det_kind(n):
+    """Algebraic shape of a node's value, for "is the force-free determinant rational at a
+    rational point" (the reference then says "Invalid (point check != 0)", else prints its
+    50-digit value, problems/force_free/validator.py:371-397).
+
+    'R'  a rational function with rational constants;
+    'C'  a constant that may be irrational (E, exp(2), sqrt(2) ...);
+    ('P', (a_1, ...), pure)  r * h_1**a_1 * ... with r, h_k rational functions and rational
+         non-integer a_k (pure: r == 1);
+    None anything else (exp/log of a coordinate expression, I ...).
+    Every derivative of r * prod h_k**a_k is prod h_k**a_k times a rational function, and the
+    determinant is homogeneous of degree 6 in u's derivatives (validator.py:323-347), so it
+    is prod h_k**(6 a_k) times a rational function: rational iff every 6 a_k is an integer.
+    """
+    k = n[0]
+    if k in ('x', 'y'):
+        return 'R'
+    if k == 'c':
+        return 'R' if len(n) == 2 else 'C'
+    if k == 'i':
+        return None
+    if k in ('neg', 'abs'):
+        return _det_kind(n[1])
+    if k in ('exp', 'log'):
+        return 'C' if _det_kind(n[1]) == 'C' else None
+    if k in ('sqrt', 'pown', 'pow'):
+        e = Fraction(1, 2) if k == 'sqrt' else (Fraction(n[2]) if k == 'pown' else _frac(n[2]))
+        kind = _det_kind(n[1])
+        if kind == 'C':
+            return 'C'
+        if kind == 'R':
+            return 'R' if e.denominator == 1 else ('P', (e,), True)
+        if isinstance(kind, tuple) and kind[2]:
+            ex = tuple(a * e for a in kind[1] if (a * e).denominator != 1)
+            return ('P', ex, True) if ex else 'R'
+        return None
+    a, b = n[1], n[2]
+    ka, kb = _det_kind(a), _det_kind(b)
+    if k in ('add', 'sub'):
+        if ka == kb and ka in ('R', 'C'):
+            return ka
+        if {ka, kb} == {'R', 'C'} and ((ka == 'R' and a[0] == 'c') or (kb == 'R' and b[0] == 'c')):
+            return 'C'
+        return None
+    if k in ('mul', 'div'):
+        if ka is None or kb is None or 'C' in (ka, kb):
+            return None          # an irrational constant factor scales det by its 6th power
+        if ka == kb == 'R':
+            return 'R'
+        ea = ka[1] if isinstance(ka, tuple) else ()
+        eb = kb[1] if isinstance(kb, tuple) else ()
+        if k == 'div':
+            eb = tuple(-x for x in eb)
+        pure = (ka == 'R' and a[0] == 'c' or isinstance(ka, tuple) and ka[2]) and \
+               (kb == 'R' and b[0] == 'c' or isinstance(kb, tuple) and kb[2])
+        return ('P', ea + eb, bool(pure))
+    return None
+
+
+def det_rational(ir) -> bool:
+    """True when the force-free determinant of this program is rational at rational points.
+    Top-level additive constants and rational constant factors do not matter (the
+    determinant sees only derivatives, and is homogeneous)."""
+    n = ir
+    while True:
+        k = n[0]
+        if k == 'neg':
+            n = n[1]
+            continue
+        if k in ('add', 'sub'):
+            a, b = n[1], n[2]
+            if a[0] == 'c' or _det_kind(a) == 'C':
+                n = b
+                continue
+            if b[0] == 'c' or _det_kind(b) == 'C':
+                n = a
+                continue
+        elif k == 'mul' and n[1][0] == 'c' and len(n[1]) == 2:
+            n = n[2]
+            continue
+        elif k in ('mul', 'div') and n[2][0] == 'c' and len(n[2]) == 2:
+            n = n[1]
+            continue
+        break
+    kind = _det_kind(n)
+    if kind in ('R', 'C'):
+        return True
+    return isinstance(kind, tuple) and all((6 * x).denominator == 1 for x in kind[1])
+
+
 def compile_ir(ir, uses_i: bool = False, rational_consts: bool = True) -> List[int]:
     em = _Emit()
     em.emit(ir)
@@ -349,8 +450,7 @@ def compile_ir(ir, uses_i: bool = False, rational_consts: bool = True) -> List[i
     xs = any(o in (PDOP['PUSH_X'], PDOP['ADD_X'], PDOP['SUB_X'], PDOP['MUL_X'], PDOP['DIV_X']) for o in ops)
     ys = any(o in (PDOP['PUSH_Y'], PDOP['ADD_Y'], PDOP['SUB_Y'], PDOP['MUL_Y'], PDOP['DIV_Y']) for o in ops)
     nonsmooth2d = xs and ys and PDOP['ABS'] in ops
-    rational = rational_consts and not uses_i and all(
-        (em.w[i] & 0xff) in _RATIONAL_OPS for i in _op_positions(em.w))
+    rational = not uses_i and det_rational(ir)
     hdr = (PDOP['HEADER'] | (em.dmax << 8) | (FLAG_COMPLEX if uses_i else 0)
            | (0 if has_coord else FLAG_NOCOORD) | (FLAG_RATIONAL if rational else 0)
            | (FLAG_NONSMOOTH2D if nonsmooth2d else 0))

@@ -3,8 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-N=${N:-65536}
-B="python bench.py --steps 1 --warmup 0 --n $N --no-cpu"
+N=${N:-262144}
+B="python bench.py --steps 1 --warmup 0 --n $N --no-cpu --no-extras"
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/pmc/trace -o run -- $B > gpurun_out/pmc/trace.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --output-format csv -d gpurun_out/pmc/sq1 -o run -- $B > gpurun_out/pmc/sq1.log 2>&1 &&

@@ -1,0 +1,86 @@
+"""Multi-rank path on the CPU: contiguous candidate shards + one all-gather of the verdict
+bitmaps (bench.py runs the same code over RCCL, one process per GPU).
+
+world_size 2 on gloo; each rank validates its shard with the CPU oracle (the per-rank engine
+stand-in -- there is no GPU here) and the gathered bitmap must equal the one-rank bitmap.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from pdeval import problem_defs as P
+from pdeval.shard import gather_verdicts, pack_bits, shard_ranges, slice_programs, unpack_bits
+
+import golden_data as G
+
+
+def test_shard_ranges_even():
+    assert shard_ranges(10, 3) == [(0, 4), (4, 7), (7, 10)]
+    assert shard_ranges(2, 4) == [(0, 1), (1, 2), (2, 2), (2, 2)]
+    assert shard_ranges(0, 2) == [(0, 0), (0, 0)]
+    r = shard_ranges(1 << 20, 8)
+    assert r[0] == (0, 131072) and r[-1][1] == 1 << 20
+
+
+def test_shard_ranges_weighted():
+    w = np.array([10, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1], dtype=float)
+    r = shard_ranges(len(w), 2, w)
+    assert r[0][0] == 0 and r[-1][1] == len(w)
+    assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+    assert r[0] == (0, 1)                      # the heavy program alone carries half the work
+    with pytest.raises(ValueError):
+        shard_ranges(3, 2, [1.0, 2.0])
+
+
+def test_slice_and_bits_roundtrip():
+    pd_ = P.force_free()
+    ops, off, _ = P.compile_strings(pd_, ['rho', 'rho*z', 'exp(z)*rho**2', 'sqrt(rho + z**2)'])
+    o2, f2 = slice_programs(ops, off, 1, 3)
+    assert f2[0] == 0 and f2[-1] == o2.size and len(f2) == 3
+    assert np.array_equal(o2, ops[off[1]:off[3]])
+    v = np.array([1, 0, 1, 1, 0, 0, 0, 1, 1], dtype=bool)
+    assert np.array_equal(unpack_bits(pack_bits(v), len(v)), v)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, strings, out_dir):
+    import torch
+    import torch.distributed as dist
+    import oracle_lib as O
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        pd_ = P.force_free()
+        ops, off, _ = P.compile_strings(pd_, strings)
+        lens = np.diff(off)
+        ranges = shard_ranges(len(strings), world, weights=lens)
+        s, e = ranges[rank]
+        o, f = slice_programs(ops, off, s, e)
+        res = O.validate(0, o, f, O.params(full_grid=0))
+        local = torch.from_numpy(pack_bits(res['status'] == 0))
+        allv = gather_verdicts(local, ranges)
+        np.save(os.path.join(out_dir, f'rank{rank}.npy'), allv)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gather_equals_single_rank(tmp_path):
+    import torch.multiprocessing as mp
+    import oracle_lib as O
+    rows = G.ref_rows('ff_d2.jsonl', 'ff_edge.jsonl')
+    strings = [r['expr'] for r in rows]
+    pd_ = P.force_free()
+    ops, off, _ = P.compile_strings(pd_, strings)
+    single = O.validate(0, ops, off, O.params(full_grid=0))['status'] == 0
+    mp.spawn(_rank_main, args=(2, _free_port(), strings, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        got = np.load(tmp_path / f'rank{r}.npy')
+        assert np.array_equal(got, single), r
+    assert single.any() and not single.all()
