@@ -112,6 +112,8 @@ typedef struct pdeval_params {
     int32_t strict_symbolic; /* 1: reproduce the reference's symbolic-stage verdict on
                                 non-smooth candidates (PDEVAL_CLS_REJECT_SYMBOLIC)       */
     int32_t reserved;
+    double noise_kappa;  /* tier 2: a failing point counts only if |residual| > noise_kappa x
+                            its first-order rounding-noise bound     */
 } pdeval_params;
 
 /* Per-candidate outputs; any pointer may be NULL (not produced).  Host or device memory
@@ -155,6 +157,19 @@ int pdeval_validate_batch(pdeval_ctx* ctx, const int32_t* ops, int64_t n_words,
 int pdeval_validate_device(pdeval_ctx* ctx, const int32_t* d_ops, int64_t n_words,
                            const int64_t* d_offsets, int64_t n, const pdeval_params* params,
                            const pdeval_outputs* d_out, void* stream, int zero_bits);
+
+/* Per-pass device timing (bench / profiling).  With timing enabled, pdeval_validate_device
+ * records a HIP event before each of its PDEVAL_N_PASSES launches and one after the last, on
+ * the launch stream (passes a problem does not run take 0 ms).  pdeval_pass_times waits for
+ * the last event of the most recent call and writes min(max_passes, PDEVAL_N_PASSES)
+ * durations in ms (and, if names != NULL, a static name per pass).                       */
+#define PDEVAL_N_PASSES 7
+int pdeval_set_timing(pdeval_ctx* ctx, int enable);
+int pdeval_pass_times(pdeval_ctx* ctx, float* ms, int max_passes, const char** names);
+/* Work-list sizes of the most recent call (synchronizes the device): [0] deferred to pass 2,
+ * [1] complex pass, [2] deferred to pass 3, [3] tier-2 entries, [4] tier-2 deep, [5] tier-2
+ * complex.                                                                                */
+int pdeval_pass_counts(pdeval_ctx* ctx, int64_t* counts, int max_counts);
 
 /* Host-side program analysis (no GPU): required stack depth, or < 0 if malformed.      */
 int pdeval_program_depth(const int32_t* ops, int64_t n_words);

@@ -29,6 +29,66 @@
 #define NC(K) (((K) + 1) * ((K) + 2) / 2)
 #define IDX(i, j) (((i) + (j)) * ((i) + (j) + 1) / 2 + (j))
 
+/* ---------------------------------------------------------------- noise bounds
+ * Tier 2 of the zero test: beside every jet value v the interpreter carries a
+ * non-negative jet E, a first-order running bound of its rounding error in units of eps:
+ * |computed - exact| <~ eps * E, coefficient-wise.  Rules (|a| = coefficient-wise modulus):
+ *   leaf x, y : 0 (exact inputs);  constant c : |c|
+ *   a +- b    : E_a + E_b + |r|
+ *   a * b     : |a| (*) E_b + E_a (*) |b| + |a| (*) |b|             ((*) = jet product)
+ *   a / b     : absdiv(E_a + |r| (*) E_b, |b|) + |r|
+ *   g(a)      : G1 (*) E_a + sum_k |f_k| |h|^k,  G1 = sum_m (m+1) |f_(m+1)| |h|^m, h = a - a0
+ * where absdiv(N, |b|) is the division recurrence with every sign made positive (it bounds
+ * the coefficients of N * (1/b)).  Real doubles for both passes (the complex pass bounds
+ * moduli). */
+static void w_mul(const double* a, const double* b, double* c, int K) {
+    double r[NCMAX];
+    for (int d = 0; d <= K; ++d)
+        for (int j = 0; j <= d; ++j) {
+            double s = 0;
+            for (int d1 = 0; d1 <= d; ++d1)
+                for (int j1 = 0; j1 <= d1; ++j1) {
+                    int d2 = d - d1, j2 = j - j1;
+                    if (j2 < 0 || j2 > d2) continue;
+                    s += a[IDX(d1 - j1, j1)] * b[IDX(d2 - j2, j2)];
+                }
+            r[IDX(d - j, j)] = s;
+        }
+    memcpy(c, r, sizeof(double) * NC(K));
+}
+
+static void w_absdiv(const double* nmr, const double* b, double* c, int K) {
+    double r[NCMAX];
+    for (int d = 0; d <= K; ++d)
+        for (int j = 0; j <= d; ++j) {
+            const int k = IDX(d - j, j);
+            double s = nmr[k];
+            for (int d1 = 1; d1 <= d; ++d1)
+                for (int j1 = 0; j1 <= d1; ++j1) {
+                    int d2 = d - d1, j2 = j - j1;
+                    if (j2 < 0 || j2 > d2) continue;
+                    s += b[IDX(d1 - j1, j1)] * r[IDX(d2 - j2, j2)];
+                }
+            r[k] = s / b[0];
+        }
+    memcpy(c, r, sizeof(double) * NC(K));
+}
+
+/* out = sum_k F[k] h^k (h[0] ignored), all non-negative */
+static void w_horner(const double* h0, const double* F, double* out, int K) {
+    double h[NCMAX], hk[NCMAX], acc[NCMAX];
+    memcpy(h, h0, sizeof(double) * NC(K));
+    h[0] = 0;
+    for (int i = 0; i < NCMAX; ++i) { acc[i] = 0; hk[i] = 0; }
+    acc[0] = F[0];
+    hk[0] = 1;
+    for (int k = 1; k <= K; ++k) {
+        w_mul(hk, h, hk, K);
+        for (int i = 0; i < NC(K); ++i) acc[i] += F[k] * hk[i];
+    }
+    memcpy(out, acc, sizeof(double) * NC(K));
+}
+
 #define S double
 #define FN(name) name##_r
 #include "jet_oracle_impl.h"
@@ -93,29 +153,46 @@ typedef struct {
     double res_abs, res_re, scale;
     int finite, grad_zero;
     double u0;
+    double noise;   /* tier 2 only: first-order rounding-noise bound of the residual */
 } pt_result;
 
+/* gamma for the finite-difference form of the first-order noise bound: the noise is
+ * (S(|c| + gamma W) - S(|c|)) * eps / gamma + eps * S, S the magnitude epilogue */
+#define NOISE_GAMMA 0x1p-30
+#define EPS64 0x1p-52
+
 static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x, double y, int cplx,
-                            int* rc) {
+                            int tier2, int* rc) {
     pt_result r = {0};
     const int K = problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
     double complex cc[NCMAX];
+    double W[NCMAX];
     if (cplx) {
-        *rc = run_c(w, nw, x, y, K, 1, cc);
+        *rc = run_c(w, nw, x, y, K, 1, cc, tier2 ? W : NULL);
     } else {
         double cr[NCMAX];
-        *rc = run_r(w, nw, x, y, K, 0, cr);
+        *rc = run_r(w, nw, x, y, K, 0, cr, tier2 ? W : NULL);
         for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
     }
     if (*rc) return r;
     int fin = 1;
-    for (int i = 0; i < NC(K); ++i) fin = fin && isfinite(creal(cc[i])) && isfinite(cimag(cc[i]));
+    for (int i = 0; i < NC(K); ++i) fin = fin && fabs(creal(cc[i])) < 0x1p160 && fabs(cimag(cc[i])) < 0x1p160;
+    /* (the device's jet_coef_ok: below 2^160, so no order-dependent overflow downstream) */
     double complex res;
     if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
         res = ff_det_c(cc, x, 0);
         r.scale = creal(ff_det_c(cc, x, 1));
     } else {
         kerr_terms(x, y, cc, cplx, &res, &r.scale);
+    }
+    if (tier2) {
+        double complex cp[NCMAX];
+        double complex res2;
+        double S2;
+        for (int i = 0; i < NC(K); ++i) cp[i] = cabs(cc[i]) + NOISE_GAMMA * W[i];
+        if (problem == PDEVAL_PROBLEM_FORCE_FREE) S2 = creal(ff_det_c(cp, x, 1));
+        else kerr_terms(x, y, cp, 0, &res2, &S2);
+        r.noise = (S2 - r.scale) * (EPS64 / NOISE_GAMMA) + EPS64 * r.scale;
     }
     r.res_abs = cabs(res);
     r.res_re = creal(res);
@@ -156,7 +233,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
         qr = 0; qmax = 0; nb = nnf = nfin = any_grad = point_reject = 0;
         for (int p = 0; p < npts && cls < 0; ++p) {
             int rc;
-            pt_result r = eval_point(problem, w, nw, px[p], py[p], cplx, &rc);
+            pt_result r = eval_point(problem, w, nw, px[p], py[p], cplx, 0, &rc);
             if (rc == -2 || rc == -3) { cls = PDEVAL_CLS_UNSUPPORTED; break; }
             if (rc) { cls = PDEVAL_CLS_BAD_PROGRAM; break; }
             for (int f = 0; f < PDEVAL_FP_N; ++f)
@@ -167,13 +244,28 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                 double v = problem == PDEVAL_PROBLEM_FORCE_FREE ? scaled(r.res_abs, r.scale) : r.res_abs;
                 if (!r.finite) {
                     if (problem == PDEVAL_PROBLEM_FORCE_FREE && !cplx) { cplx = 1; goto again; }
-                    point_reject = 1;
+                    point_reject = 2;    /* non-finite at a reference point: final */
                 } else if (!(qr >= v)) {
                     qr = v;
                 }
                 if (p == nref - 1) {
-                    if (problem == PDEVAL_PROBLEM_FORCE_FREE) point_reject = point_reject || !(qr <= prm->tau_point);
-                    else point_reject = point_reject || !(qr < prm->kerr_abs_tol);
+                    if (!point_reject) {
+                        if (problem == PDEVAL_PROBLEM_FORCE_FREE) point_reject = !(qr <= prm->tau_point);
+                        else point_reject = !(qr < prm->kerr_abs_tol);
+                    }
+                    if (point_reject == 1) {
+                        /* tier 2: a point-stage failure stands only where the residual also
+                         * exceeds its rounding-noise bound */
+                        point_reject = 0;
+                        for (int p2 = 0; p2 < nref; ++p2) {
+                            int rc2;
+                            pt_result r2 = eval_point(problem, w, nw, px[p2], py[p2], cplx, 1, &rc2);
+                            double v2 = problem == PDEVAL_PROBLEM_FORCE_FREE ? scaled(r2.res_abs, r2.scale) : r2.res_abs;
+                            int fails = problem == PDEVAL_PROBLEM_FORCE_FREE ? !(v2 <= prm->tau_point)
+                                                                             : !(v2 < prm->kerr_abs_tol);
+                            if (fails && r2.res_abs > prm->noise_kappa * r2.noise) point_reject = 1;
+                        }
+                    }
                     if (point_reject && !prm->full_grid) cls = PDEVAL_CLS_REJECT_POINT;
                 }
                 continue;
@@ -186,6 +278,17 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                 if (!r.grad_zero) any_grad = 1;
             } else {
                 ++nnf;
+            }
+        }
+        if (cls < 0 && !point_reject && nb > prm->max_bad) {
+            /* tier 2 of the grid stage: count only points whose residual also exceeds its
+             * rounding-noise bound */
+            nb = 0;
+            for (int p = nref; p < npts; ++p) {
+                int rc2;
+                pt_result r2 = eval_point(problem, w, nw, px[p], py[p], cplx, 1, &rc2);
+                if (rc2 || !r2.finite) continue;
+                if (scaled(r2.res_abs, r2.scale) > prm->tau_grid && r2.res_abs > prm->noise_kappa * r2.noise) ++nb;
             }
         }
         if (cls < 0) {
@@ -215,12 +318,24 @@ int oracle_jet(int problem, const int32_t* w, int64_t nw, double x, double y, in
     double complex cc[NCMAX];
     int rc;
     if (cplx) {
-        rc = run_c(w, nw, x, y, K, 1, cc);
+        rc = run_c(w, nw, x, y, K, 1, cc, NULL);
     } else {
         double cr[NCMAX];
-        rc = run_r(w, nw, x, y, K, 0, cr);
+        rc = run_r(w, nw, x, y, K, 0, cr, NULL);
         for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
     }
     for (int i = 0; i < NC(K) && !rc; ++i) { re[i] = creal(cc[i]); im[i] = cimag(cc[i]); }
+    return rc;
+}
+
+/* One point with the tier-2 noise bound: out = {|res|, S, noise, finite} (for unit tests and
+ * threshold calibration). */
+int oracle_point(int problem, const int32_t* w, int64_t nw, double x, double y, int cplx, double* out) {
+    int rc;
+    pt_result r = eval_point(problem, w, nw, x, y, cplx, 1, &rc);
+    out[0] = r.res_abs;
+    out[1] = r.scale;
+    out[2] = r.noise;
+    out[3] = r.finite;
     return rc;
 }

@@ -71,8 +71,15 @@ static S FN(spow)(S x, double a, int cplx_pass) {
     return cexp(a * clog(x));
 }
 
-static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, int cplx_pass, S* out) {
+static void FN(wabs)(const S* v, double* w, int K) { for (int i = 0; i < NC(K); ++i) w[i] = cabs(v[i]); }
+
+/* Evaluate a program at (px, py).  eout != NULL: also carry the first-order rounding-error
+ * jet E (rules at w_mul in jet_oracle.c) and return it. */
+static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, int cplx_pass, S* out,
+                   double* eout) {
     S st[16][NCMAX];
+    double es[16][NCMAX];
+    const int trk = eout != NULL;
     int d = 0;
     for (int64_t pc = 1; pc < nw;) {
         uint32_t word = (uint32_t)w[pc], op = word & 0xffu;
@@ -87,63 +94,130 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
         }
         S* t = d > 0 ? st[d - 1] : NULL;
         S* u = d > 1 ? st[d - 2] : NULL;
-        S f[KMAX + 1];
+        double* et = d > 0 ? es[d - 1] : NULL;
+        double* eu = d > 1 ? es[d - 2] : NULL;
+        S f[KMAX + 2];
+        double A[NCMAX], B[NCMAX], R[NCMAX], T1[NCMAX], T2[NCMAX];
         switch (op) {
-            case PDOP_PUSH_X: FN(jconst)(st[d], px); st[d][IDX(1, 0)] = 1; ++d; break;
-            case PDOP_PUSH_Y: FN(jconst)(st[d], py); st[d][IDX(0, 1)] = 1; ++d; break;
-            case PDOP_PUSH_C: FN(jconst)(st[d], imm); ++d; break;
-            case PDOP_PUSH_I:
-                if (!cplx_pass) return -2;
-                FN(jconst)(st[d], I); ++d; break;
-            case PDOP_ADD: for (int i = 0; i < NC(K); ++i) u[i] = u[i] + t[i]; --d; break;
-            case PDOP_SUB: for (int i = 0; i < NC(K); ++i) u[i] = u[i] - t[i]; --d; break;
-            case PDOP_RSUB: for (int i = 0; i < NC(K); ++i) u[i] = t[i] - u[i]; --d; break;
-            case PDOP_MUL: FN(jmul)(u, t, u, K); --d; break;
-            case PDOP_DIV: FN(jdiv)(u, t, u, K); --d; break;
-            case PDOP_RDIV: FN(jdiv)(t, u, u, K); --d; break;
-            case PDOP_ADDC: t[0] += imm; break;
-            case PDOP_MULC: for (int i = 0; i < NC(K); ++i) t[i] *= imm; break;
-            case PDOP_RDIVC: { S c[NCMAX]; FN(jconst)(c, imm); FN(jdiv)(c, t, t, K); break; }
+            case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I:
+                if (op == PDOP_PUSH_X) { FN(jconst)(st[d], px); st[d][IDX(1, 0)] = 1; }
+                else if (op == PDOP_PUSH_Y) { FN(jconst)(st[d], py); st[d][IDX(0, 1)] = 1; }
+                else if (op == PDOP_PUSH_C) FN(jconst)(st[d], imm);
+                else { if (!cplx_pass) return -2; FN(jconst)(st[d], I); }
+                if (trk) {
+                    for (int i = 0; i < NCMAX; ++i) es[d][i] = 0;
+                    if (op == PDOP_PUSH_C) es[d][0] = fabs(imm);
+                }
+                ++d;
+                break;
+            case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB:
+                for (int i = 0; i < NC(K); ++i)
+                    u[i] = op == PDOP_ADD ? u[i] + t[i] : (op == PDOP_SUB ? u[i] - t[i] : t[i] - u[i]);
+                if (trk) for (int i = 0; i < NC(K); ++i) eu[i] += et[i] + cabs(u[i]);
+                --d;
+                break;
+            case PDOP_MUL:
+                if (trk) {
+                    FN(wabs)(u, A, K); FN(wabs)(t, B, K);
+                    w_mul(A, et, T1, K); w_mul(eu, B, T2, K); w_mul(A, B, R, K);
+                    for (int i = 0; i < NC(K); ++i) eu[i] = T1[i] + T2[i] + R[i];
+                }
+                FN(jmul)(u, t, u, K);
+                --d;
+                break;
+            case PDOP_DIV: case PDOP_RDIV: {
+                const double* en = op == PDOP_DIV ? eu : et;
+                const double* ed = op == PDOP_DIV ? et : eu;
+                if (trk) { memcpy(T1, en, sizeof T1); memcpy(T2, ed, sizeof T2); FN(wabs)(op == PDOP_DIV ? t : u, B, K); }
+                FN(jdiv)(op == PDOP_DIV ? u : t, op == PDOP_DIV ? t : u, u, K);
+                if (trk) {
+                    FN(wabs)(u, R, K);
+                    w_mul(R, T2, A, K);
+                    for (int i = 0; i < NC(K); ++i) A[i] += T1[i];
+                    w_absdiv(A, B, eu, K);
+                    for (int i = 0; i < NC(K); ++i) eu[i] += R[i];
+                }
+                --d;
+                break;
+            }
+            case PDOP_ADDC: t[0] += imm; if (trk) et[0] += fabs(imm) + cabs(t[0]); break;
+            case PDOP_MULC:
+                for (int i = 0; i < NC(K); ++i) t[i] *= imm;
+                if (trk) for (int i = 0; i < NC(K); ++i) et[i] = et[i] * fabs(imm) + cabs(t[i]);
+                break;
+            case PDOP_RDIVC: {
+                S c[NCMAX];
+                FN(jconst)(c, imm);
+                if (trk) { memcpy(T2, et, sizeof T2); FN(wabs)(t, B, K); }
+                FN(jdiv)(c, t, t, K);
+                if (trk) {
+                    FN(wabs)(t, R, K);
+                    w_mul(R, T2, A, K);
+                    A[0] += fabs(imm);
+                    w_absdiv(A, B, et, K);
+                    for (int i = 0; i < NC(K); ++i) et[i] += R[i];
+                }
+                break;
+            }
             case PDOP_NEG: for (int i = 0; i < NC(K); ++i) t[i] = -t[i]; break;
-            case PDOP_ADD_X: t[0] += px; t[IDX(1, 0)] += 1; break;
-            case PDOP_ADD_Y: t[0] += py; t[IDX(0, 1)] += 1; break;
-            case PDOP_SUB_X: t[0] -= px; t[IDX(1, 0)] -= 1; break;
-            case PDOP_SUB_Y: t[0] -= py; t[IDX(0, 1)] -= 1; break;
+            case PDOP_ADD_X: t[0] += px; t[IDX(1, 0)] += 1; if (trk) et[0] += cabs(t[0]); break;
+            case PDOP_ADD_Y: t[0] += py; t[IDX(0, 1)] += 1; if (trk) et[0] += cabs(t[0]); break;
+            case PDOP_SUB_X: t[0] -= px; t[IDX(1, 0)] -= 1; if (trk) et[0] += cabs(t[0]); break;
+            case PDOP_SUB_Y: t[0] -= py; t[IDX(0, 1)] -= 1; if (trk) et[0] += cabs(t[0]); break;
             case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: {
                 S v[NCMAX];
                 int isx = (op == PDOP_MUL_X || op == PDOP_DIV_X);
                 FN(jconst)(v, isx ? px : py);
                 v[isx ? IDX(1, 0) : IDX(0, 1)] = 1;
-                if (op == PDOP_MUL_X || op == PDOP_MUL_Y) FN(jmul)(t, v, t, K);
-                else FN(jdiv)(t, v, t, K);
+                if (trk) { FN(wabs)(v, B, K); memcpy(T1, et, sizeof T1); }
+                if (op == PDOP_MUL_X || op == PDOP_MUL_Y) {
+                    FN(jmul)(t, v, t, K);
+                    if (trk) { w_mul(T1, B, et, K); FN(wabs)(t, R, K); for (int i = 0; i < NC(K); ++i) et[i] += R[i]; }
+                } else {
+                    FN(jdiv)(t, v, t, K);
+                    if (trk) { FN(wabs)(t, R, K); w_absdiv(T1, B, et, K); for (int i = 0; i < NC(K); ++i) et[i] += R[i]; }
+                }
                 break;
             }
             case PDOP_POWN: {
                 int n = (int)((word >> 8) & 0xffu);
                 S b[NCMAX];
+                double eb[NCMAX];
                 memcpy(b, t, sizeof(S) * NC(K));
-                for (int k = 1; k < n; ++k) FN(jmul)(t, b, t, K);
+                if (trk) { memcpy(eb, et, sizeof eb); FN(wabs)(b, B, K); }
+                for (int k = 1; k < n; ++k) {
+                    if (trk) {
+                        FN(wabs)(t, A, K);
+                        w_mul(A, eb, T1, K); w_mul(et, B, T2, K); w_mul(A, B, R, K);
+                        for (int i = 0; i < NC(K); ++i) et[i] = T1[i] + T2[i] + R[i];
+                    }
+                    FN(jmul)(t, b, t, K);
+                }
                 break;
             }
-            case PDOP_POW: case PDOP_SQRT: {
-                double a = (op == PDOP_SQRT) ? 0.5 : imm;
+            case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: {
                 S x0 = t[0];
-                f[0] = FN(spow)(x0, a, cplx_pass);
-                for (int k = 1; k <= K; ++k) f[k] = f[k - 1] * ((a - (k - 1)) / k) / x0;
-                FN(jcompose)(t, f, K);
-                break;
-            }
-            case PDOP_EXP: {
-                S e = cplx_pass ? cexp(t[0]) : exp(creal(t[0]));
-                double fact = 1;
-                for (int k = 0; k <= K; ++k) { if (k) fact *= k; f[k] = e / fact; }
-                FN(jcompose)(t, f, K);
-                break;
-            }
-            case PDOP_LOG: {
-                S x0 = t[0];
-                f[0] = cplx_pass ? clog(x0) : (creal(x0) > 0 ? log(creal(x0)) : (creal(x0) == 0 ? -INFINITY : NAN));
-                for (int k = 1; k <= K; ++k) f[k] = ((k & 1) ? 1.0 : -1.0) / (k * FN(spow)(x0, k, cplx_pass));
+                if (op == PDOP_POW || op == PDOP_SQRT) {
+                    double a = (op == PDOP_SQRT) ? 0.5 : imm;
+                    f[0] = FN(spow)(x0, a, cplx_pass);
+                    for (int k = 1; k <= K + 1; ++k) f[k] = f[k - 1] * ((a - (k - 1)) / k) / x0;
+                } else if (op == PDOP_EXP) {
+                    S e = cplx_pass ? cexp(x0) : exp(creal(x0));
+                    double fact = 1;
+                    for (int k = 0; k <= K + 1; ++k) { if (k) fact *= k; f[k] = e / fact; }
+                } else {
+                    f[0] = cplx_pass ? clog(x0) : (creal(x0) > 0 ? log(creal(x0)) : (creal(x0) == 0 ? -INFINITY : NAN));
+                    for (int k = 1; k <= K + 1; ++k) f[k] = ((k & 1) ? 1.0 : -1.0) / (k * FN(spow)(x0, k, cplx_pass));
+                }
+                if (trk) {
+                    double G[KMAX + 1], Fa[KMAX + 1];
+                    for (int k = 0; k <= K; ++k) { G[k] = (k + 1) * cabs(f[k + 1]); Fa[k] = cabs(f[k]); }
+                    FN(wabs)(t, A, K);
+                    w_horner(A, G, T1, K);         /* G1 = sum (m+1)|f_(m+1)| |h|^m */
+                    w_horner(A, Fa, R, K);         /* sum |f_k| |h|^k */
+                    w_mul(T1, et, T2, K);
+                    for (int i = 0; i < NC(K); ++i) et[i] = T2[i] + R[i];
+                }
                 FN(jcompose)(t, f, K);
                 break;
             }
@@ -161,6 +235,7 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
     }
     if (d != 1) return -5;
     memcpy(out, st[0], sizeof(S) * NC(K));
+    if (trk) memcpy(eout, es[0], sizeof(double) * NC(K));
     return 0;
 }
 

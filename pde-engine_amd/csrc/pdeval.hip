@@ -15,6 +15,7 @@
 
 #include "../../include/pdeval.h"
 #include "pdeval_kernels.h"
+#include "pdeval_tier2.h"
 
 using namespace pd;
 
@@ -36,7 +37,10 @@ struct pdeval_ctx {
     int64_t* d_defer = nullptr;   // pass 1 -> pass 2 (stack 3..4)
     int64_t* d_defer2 = nullptr;  // pass 2 -> pass 3 (stack 5..8)
     int64_t* d_cplx = nullptr;
-    int32_t* d_counts = nullptr;  // [0] defer, [1] cplx, [2] defer2
+    int64_t* d_esc = nullptr;       // tier-2 escalations, real passes
+    int64_t* d_esc_deep = nullptr;  // tier-2 entries deeper than the first tier-2 variant
+    int64_t* d_esc_c = nullptr;     // tier-2 escalations of the complex pass
+    int32_t* d_counts = nullptr;  // [0] defer, [1] cplx, [2] defer2, [3] esc, [4] esc_deep, [5] esc_c
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -44,7 +48,16 @@ struct pdeval_ctx {
     uint8_t* d_outbuf = nullptr;
     int64_t outbuf_bytes = 0;
     std::string err;
+    // optional per-pass timing (pdeval_set_timing): an event before every pass and one after
+    // the last, recorded on the launch stream
+    bool timing = false;
+    hipEvent_t ev[PDEVAL_N_PASSES + 1] = {};
+    int ev_recorded = 0;
 };
+
+static const char* const kPassNames[PDEVAL_N_PASSES] = {
+    "pass1_stack2", "pass2_stack4", "pass3_stack8", "pass4_complex",
+    "tier2_stack2", "tier2_stack8", "tier2_complex"};
 
 static thread_local std::string g_err;
 
@@ -171,7 +184,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
         if ((e = hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
             return fail("hipMemcpy", e);
     }
-    if ((e = hipMalloc(&c->d_counts, 4 * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc(&c->d_counts, 8 * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
     *out = c;
     return PDEVAL_OK;
 }
@@ -181,8 +194,11 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc, (void*)c->d_defer, (void*)c->d_defer2, (void*)c->d_cplx,
+                    (void*)c->d_esc, (void*)c->d_esc_deep, (void*)c->d_esc_c,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) hipFree(p);
+    for (hipEvent_t& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return PDEVAL_OK;
@@ -203,6 +219,7 @@ extern "C" int pdeval_default_params(int problem_id, pdeval_params* p) {
     p->max_bad = 0;
     p->strict_symbolic = 1;
     p->reserved = 0;
+    p->noise_kappa = 16.0;  // true zeros <= 0.4, real residuals >= 1e8 x noise
     (void)problem_id;
     return PDEVAL_OK;
 }
@@ -288,7 +305,7 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
 // ---------------------------------------------------------------------------- launches
 static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (n <= c->cap) return PDEVAL_OK;
-    for (int64_t** p : {&c->d_defer, &c->d_defer2, &c->d_cplx}) {
+    for (int64_t** p : {&c->d_defer, &c->d_defer2, &c->d_cplx, &c->d_esc, &c->d_esc_deep, &c->d_esc_c}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -297,6 +314,9 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     HIPCHK(c, hipMalloc(&c->d_defer, cap * sizeof(int64_t)));
     HIPCHK(c, hipMalloc(&c->d_defer2, cap * sizeof(int64_t)));
     HIPCHK(c, hipMalloc(&c->d_cplx, cap * sizeof(int64_t)));
+    HIPCHK(c, hipMalloc(&c->d_esc, cap * sizeof(int64_t)));
+    HIPCHK(c, hipMalloc(&c->d_esc_deep, cap * sizeof(int64_t)));
+    HIPCHK(c, hipMalloc(&c->d_esc_c, cap * sizeof(int64_t)));
     c->cap = cap;
     return PDEVAL_OK;
 }
@@ -306,9 +326,17 @@ template <class T, int K, int MAXD> constexpr size_t stack_lds(int waves) {
     return (size_t)waves * (MAXD - 1) * ((K + 1) * (K + 2) / 2) * 64 * sizeof(T);
 }
 
+// dynamic LDS of one tier-2 wave: (MAXD-1) slots of a value jet (T) and an error jet (f64)
+template <class T, int K, int MAXD> constexpr size_t tier2_lds() {
+    return (size_t)(MAXD - 1) * ((K + 1) * (K + 2) / 2) * 64 * (sizeof(T) + sizeof(double));
+}
+
 template <int PROB>
 static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, const int64_t* d_off, int64_t n,
                       const pdeval_params& prm, const pdeval_outputs& o, hipStream_t s) {
+    auto mark = [&](int k) {
+        if (c->timing) (void)hipEventRecord(c->ev[k], s);
+    };
     KernelArgs a{};
     a.ops = d_ops;
     a.offsets = d_off;
@@ -333,7 +361,9 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.cplx_list = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? c->d_cplx : nullptr;
     a.cplx_count = c->d_counts + 1;
     a.list_capacity = c->cap;
-    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, 4 * sizeof(int32_t), s));
+    a.esc_list = c->d_esc;
+    a.esc_count = c->d_counts + 3;
+    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, 8 * sizeof(int32_t), s));
     constexpr int WPB = 4;  // waves (candidates) per 256-thread block
     const int64_t blocks = (n + WPB - 1) / WPB;
     // pass 1: programs whose stack fits 2 jets (>92 % of force-free depth 4), one wave per
@@ -341,6 +371,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.defer_list = c->d_defer;
     a.defer_count = c->d_counts + 0;
     constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    mark(0);
     hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256),
                        (stack_lds<double, K, 2>(4)), s, a);
     HIPCHK(c, hipGetLastError());
@@ -353,6 +384,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     b.defer_count = c->d_counts + 2;
     const int64_t pblocks = std::min<int64_t>(blocks, 2048);
     // follow-up passes: one wave per block (their LDS stacks are deeper)
+    mark(1);
     hipLaunchKernelGGL((validate_kernel<PROB, double, 4, true>), dim3((unsigned)(4 * pblocks)), dim3(64),
                        (stack_lds<double, K, 4>(1)), s, b);
     HIPCHK(c, hipGetLastError());
@@ -361,22 +393,61 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     b2.list = c->d_defer2;
     b2.list_count = c->d_counts + 2;
     b2.defer_list = nullptr;
+    mark(2);
     hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
                        dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
                        (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, b2);
     HIPCHK(c, hipGetLastError());
-    if (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
         // pass 4: candidates not real at the reference point, in complex arithmetic
         KernelArgs x = a;
         x.list = c->d_cplx;
         x.list_count = c->d_counts + 1;
         x.cplx_list = nullptr;
         x.defer_list = nullptr;
+        x.esc_list = c->d_esc_c;
+        x.esc_count = c->d_counts + 5;
         const int64_t cblocks = std::min<int64_t>(blocks, 2048);
+        mark(3);
         hipLaunchKernelGGL((validate_kernel<PROB, cplx, 4, true>), dim3((unsigned)(4 * cblocks)),
                            dim3(64), (stack_lds<cplx, K, 4>(1)), s, x);
         HIPCHK(c, hipGetLastError());
+    } else {
+        mark(3);
     }
+    // tier 2 (pdeval_tier2.h): re-decide every tier-1 failure with error bounds.  Stack <= 2
+    // first; deeper programs go on to the MAXD = 8 variant; complex candidates separately.
+    KernelArgs t = a;
+    t.list = c->d_esc;
+    t.list_count = c->d_counts + 3;
+    t.defer_list = c->d_esc_deep;
+    t.defer_count = c->d_counts + 4;
+    mark(4);
+    hipLaunchKernelGGL((tier2_kernel<PROB, double, 2>), dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(64),
+                       (tier2_lds<double, K, 2>()), s, t);
+    HIPCHK(c, hipGetLastError());
+    KernelArgs t2 = a;
+    t2.list = c->d_esc_deep;
+    t2.list_count = c->d_counts + 4;
+    t2.defer_list = nullptr;
+    mark(5);
+    hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
+                       dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, t2);
+    HIPCHK(c, hipGetLastError());
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+        KernelArgs tc = a;
+        tc.list = c->d_esc_c;
+        tc.list_count = c->d_counts + 5;
+        tc.defer_list = nullptr;
+        mark(6);
+        hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4>), dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(64),
+                           (tier2_lds<cplx, K, 4>()), s, tc);
+        HIPCHK(c, hipGetLastError());
+    } else {
+        mark(6);
+    }
+    mark(PDEVAL_N_PASSES);
+    c->ev_recorded = c->timing ? 1 : 0;
     return PDEVAL_OK;
 }
 
@@ -480,5 +551,42 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
     if ((rc = dl(out->n_bad, d.n_bad, 4 * n))) return rc;
     if ((rc = dl(out->n_nonfinite, d.n_nonfinite, 4 * n))) return rc;
     HIPCHK(c, hipStreamSynchronize(s));
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_set_timing(pdeval_ctx* c, int enable) {
+    if (!c) return PDEVAL_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (enable && !c->ev[0])
+        for (hipEvent_t& e : c->ev) HIPCHK(c, hipEventCreate(&e));
+    c->timing = enable != 0;
+    c->ev_recorded = 0;
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_pass_times(pdeval_ctx* c, float* ms, int max_passes, const char** names) {
+    if (!c || !ms || max_passes < 0) return PDEVAL_ERR_ARG;
+    if (!c->ev_recorded) {
+        c->err = "pdeval_pass_times: no timed call (pdeval_set_timing(ctx, 1) first)";
+        return PDEVAL_ERR_ARG;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipEventSynchronize(c->ev[PDEVAL_N_PASSES]));
+    const int n = max_passes < PDEVAL_N_PASSES ? max_passes : PDEVAL_N_PASSES;
+    for (int k = 0; k < n; ++k) {
+        HIPCHK(c, hipEventElapsedTime(&ms[k], c->ev[k], c->ev[k + 1]));
+        if (names) names[k] = kPassNames[k];
+    }
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_pass_counts(pdeval_ctx* c, int64_t* counts, int max_counts) {
+    if (!c || !counts || max_counts < 0) return PDEVAL_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    int32_t h[8] = {0};
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(h, c->d_counts, sizeof(h), hipMemcpyDeviceToHost));
+    for (int k = 0; k < max_counts && k < 8; ++k) counts[k] = h[k];
     return PDEVAL_OK;
 }

@@ -45,7 +45,20 @@ struct KernelArgs {
     int64_t* cplx_list;         // FF candidates non-finite at the reference point
     int32_t* cplx_count;
     int64_t list_capacity;      // capacity of defer_list and cplx_list (appends beyond are dropped)
+    int64_t* esc_list;          // tier-2 escalations: cand | ESC_* flags << 48
+    int32_t* esc_count;
 };
+
+// Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).
+enum : uint32_t {
+    ESC_POINT = 1,      // the point stage failed its scaled test (tier 1)
+    ESC_GRID_EVAL = 2,  // the grid was evaluated in tier 1 (full_grid, or the point passed)
+    ESC_GRID_FAIL = 4,  // ... and had more than max_bad failing points
+    ESC_ANY_GRAD = 8,   // tier 1 saw a finite point with a non-zero gradient
+    ESC_NFIN = 16,      // tier 1 saw at least one finite grid point
+};
+#define PD_ESC_SHIFT 48
+#define PD_ESC_CAND_MASK ((1ll << PD_ESC_SHIFT) - 1)
 
 // Append a candidate to a device work list (lane 0 only).  Returns false when the list is
 // full -- impossible when capacity >= n, which the host guarantees; checked anyway so a bad
@@ -285,6 +298,12 @@ template <int K> __device__ __forceinline__ void absj(typename JetOps<cplx, K>::
 }
 
 // ------------------------------------------------------------------ residual epilogues
+// A sample point counts as finite only if every Taylor coefficient of u is below 2^160: the
+// residual is then free of intermediate overflow in any evaluation order (force-free S is of
+// degree 6 in the coefficients), so the device and the oracle agree on which points exist.
+constexpr double kHugeJet = 0x1p160;
+__device__ __forceinline__ bool jet_coef_ok(double v) { return fabs(v) < kHugeJet; }
+__device__ __forceinline__ bool jet_coef_ok(cplx v) { return fabs(v.re) < kHugeJet && fabs(v.im) < kHugeJet; }
 struct PointResult {
     double res_re, res_im;  // residual (complex pass: both parts)
     double res_abs;         // |residual|
@@ -406,7 +425,7 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u
     r.grad_zero = is_zero(u[ji(1, 0)]) && is_zero(u[ji(0, 1)]);
     bool fin = finite_(det) && isfinite(S);
 #pragma unroll
-    for (int i = 0; i < 15; ++i) fin = fin && finite_(u[i]);
+    for (int i = 0; i < 15; ++i) fin = fin && jet_coef_ok(u[i]);
     r.finite = fin;
     return r;
 }
@@ -431,7 +450,7 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue(const T*
     r.grad_zero = is_zero(u[ji(1, 0)]) && is_zero(u[ji(0, 1)]);
     bool fin = finite_(L) && isfinite(r.scale);
 #pragma unroll
-    for (int i = 0; i < 6; ++i) fin = fin && finite_(u[i]);
+    for (int i = 0; i < 6; ++i) fin = fin && jet_coef_ok(u[i]);
     r.finite = fin;
     return r;
 }
@@ -647,6 +666,8 @@ __global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(Kernel
         }
         double q_ref = 0.0;        // FF: q*, Kerr: max |lhs| over reference points
         bool point_reject = false;
+        bool point_final = false;  // non-finite at a reference point: no tier 2
+        bool grid_eval = true;
         double qmax = 0.0;
         int nbad = 0, nnonfin = 0, nfin = 0;
         bool grad_nz = false;
@@ -719,7 +740,7 @@ __global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(Kernel
                             if (lane == 0 && a.cplx_list)
                                 list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
                         } else {
-                            point_reject = true;  // not finite even in the complex field
+                            point_reject = point_final = true;  // not finite even in the complex field
                         }
                     } else {
                         point_reject = !(q_ref <= a.prm.tau_point);
@@ -727,9 +748,13 @@ __global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(Kernel
                 } else {
                     // Kerr fast point check (kerr validator.py:163-192): non-real / NaN at a
                     // reference point rejects; otherwise reject iff max|lhs| >= 1e-10 (absolute)
+                    point_final = nf;
                     point_reject = nf || !(q_ref < a.prm.kerr_abs_tol);
                 }
-                if (status < 0 && point_reject && !a.prm.full_grid) status = PDEVAL_CLS_REJECT_POINT;
+                if (point_reject && !a.prm.full_grid) {
+                    grid_eval = false;   // the reference's control flow: stop after the point stage
+                    break;
+                }
             }
         }
         // wave reductions
@@ -747,12 +772,29 @@ __global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(Kernel
                 // non-constant u goes on and its det is identically 0.  Kerr excludes every
                 // u that simplify() reduces to a constant (kerr validator.py:231-240).
                 const bool structural = (PROB != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);
+                uint32_t esc = 0;
                 if (!any_grad && nfin > 0 && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
-                else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;
-                else if (nbad > a.prm.max_bad) cls = PDEVAL_CLS_REJECT_GRID;
-                else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic &&
-                         (hdr & PDEVAL_FLAG_NONSMOOTH2D)) cls = PDEVAL_CLS_REJECT_SYMBOLIC;
-                else cls = PDEVAL_CLS_ACCEPT;
+                else if (point_reject) {
+                    cls = PDEVAL_CLS_REJECT_POINT;
+                    if (!point_final)
+                        esc = ESC_POINT | (grid_eval ? ESC_GRID_EVAL : 0u) |
+                              (grid_eval && nbad > a.prm.max_bad ? ESC_GRID_FAIL : 0u);
+                } else if (nbad > a.prm.max_bad) {
+                    cls = PDEVAL_CLS_REJECT_GRID;
+                    esc = ESC_GRID_EVAL | ESC_GRID_FAIL;
+                } else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic &&
+                           (hdr & PDEVAL_FLAG_NONSMOOTH2D)) {
+                    cls = PDEVAL_CLS_REJECT_SYMBOLIC;
+                } else {
+                    cls = PDEVAL_CLS_ACCEPT;
+                }
+                // a tier-1 failure may be rounding noise: tier 2 re-decides it with error
+                // bounds (tier2_kernel); the class written here is provisional
+                if (esc && a.esc_list) {
+                    esc |= (any_grad ? ESC_ANY_GRAD : 0u) | (nfin > 0 ? ESC_NFIN : 0u);
+                    list_append(a.esc_list, a.esc_count, a.list_capacity,
+                                cand | ((int64_t)esc << PD_ESC_SHIFT));
+                }
             }
             if (a.out.status) a.out.status[cand] = (uint8_t)cls;
             if (a.out.q_ref) a.out.q_ref[cand] = q_ref;

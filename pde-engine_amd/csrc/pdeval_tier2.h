@@ -1,0 +1,436 @@
+// pdeval_tier2.h -- tier 2 of the zero test: re-decide tier-1 failures with error bounds.
+//
+// Tier 1 (validate_kernel) rejects a sample point when the scaled residual q = |res| / S
+// exceeds a threshold.  S bounds the magnitude of the residual's monomials, but not the
+// rounding noise of the jet coefficients they are built from: a true solution whose jets
+// carry noise in coefficients that are exactly zero (u = z*(-(rho/z + 1)) = -rho - z, whose
+// second derivatives are rounding noise) or that sits near a pole can show q ~ 1 at some
+// points.  The reference decides these exactly (problems/force_free/validator.py:349-427),
+// so every tier-1 failure is re-evaluated here with a first-order running error bound E
+// carried beside every jet (|computed - exact| <~ eps * E, coefficient-wise):
+//   leaf x, y : 0          constant c : |c|
+//   a +- b    : E_a + E_b + |r|
+//   a * b     : |a| (*) (E_b + |b|) + E_a (*) |b|          ((*) = jet product)
+//   a / b     : absdiv(E_a + |r| (*) E_b, |b|) + |r|
+//   g(a)      : G1 (*) E_a + sum_k |f_k| |h|^k,   G1 = sum_m (m+1) |f_(m+1)| |h|^m
+// (absdiv = the division recurrence with every sign positive).  The residual's noise is the
+// first-order sensitivity of the magnitude epilogue: noise = (S(|u| + g E) - S(|u|)) eps/g
+// + eps S.  A point fails in tier 2 only if it fails tier 1 AND |res| > noise_kappa * noise.
+// The CPU oracle (oracle/jet_oracle_impl.h) carries the same bound.
+#pragma once
+#include "pdeval_kernels.h"
+
+namespace pd {
+
+constexpr double kNoiseGamma = 0x1p-30;
+constexpr double kEps = 0x1p-52;
+
+template <int K> struct EJ {
+    static constexpr int NC = nc(K);
+    // c = a (*) b, non-negative jets (c may alias a or b)
+    static PD_HD void mul(const double* a, const double* b, double* c) {
+        double r[NC];
+        jmul<double, K, K, K>(a, b, r);
+#pragma unroll
+        for (int i = 0; i < NC; ++i) c[i] = r[i];
+    }
+    // c = absdiv(n, b): c_k = (n_k + sum_{j>=1} b_j c_(k-j)) / b_0  (c may alias n)
+    static PD_HD void absdiv(const double* n, const double* b, double* c) {
+        const double inv = 1.0 / b[0];
+#pragma unroll
+        for (int d = 0; d <= K; ++d)
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                double s = n[ji(d - j, j)];
+#pragma unroll
+                for (int d1 = 1; d1 <= d; ++d1)
+#pragma unroll
+                    for (int j1 = 0; j1 <= d1; ++j1) {
+                        const int d2 = d - d1, j2 = j - j1;
+                        if (j2 < 0 || j2 > d2) continue;
+                        s = fma(b[ji(d1 - j1, j1)], c[ji(d2 - j2, j2)], s);
+                    }
+                c[ji(d - j, j)] = s * inv;
+            }
+    }
+    template <class T> static PD_HD void absv(const T* v, double* w) {
+#pragma unroll
+        for (int i = 0; i < NC; ++i) w[i] = mag(v[i]);
+    }
+    template <class T> static PD_HD void add_abs(const T* v, double* e) {
+#pragma unroll
+        for (int i = 0; i < NC; ++i) e[i] += mag(v[i]);
+    }
+};
+
+// Taylor coefficients f[0..K+1] of the outer function of a composition opcode at x0, as the
+// tier-1 JetOps compute f[0..K] (the value path itself is JetOps, unchanged).
+template <class T, int K> __device__ __forceinline__ void outer_coefs(uint32_t op, T x0, double alpha, T* f) {
+    if (op == PDOP_EXP) {
+        f[0] = exp_(x0);
+#pragma unroll
+        for (int k = 1; k <= K + 1; ++k) f[k] = f[k - 1] * (1.0 / k);
+    } else if (op == PDOP_LOG) {
+        const T r = recip(x0);
+        f[0] = log_(x0);
+        T rk = r;
+#pragma unroll
+        for (int k = 1; k <= K + 1; ++k) {
+            f[k] = rk * (((k & 1) ? 1.0 : -1.0) / k);
+            rk = rk * r;
+        }
+    } else {
+        const double a = op == PDOP_SQRT ? 0.5 : alpha;
+        const T f0 = op == PDOP_SQRT ? sqrt_(x0) : pow_real_exp(x0, a);
+        const T r = recip(x0);
+        f[0] = f0;
+#pragma unroll
+        for (int k = 1; k <= K + 1; ++k) f[k] = f[k - 1] * r * ((a - (k - 1)) / k);
+    }
+}
+
+template <class T, int K, int MAXD> struct ErrInterp {
+    using O = JetOps<T, K>;
+    using J = typename O::J;
+    using E = EJ<K>;
+    static constexpr int NC = nc(K);
+
+    static __device__ __forceinline__ void st(T* vs, double* es, int slot, int lane, const J& t, const double* e) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            vs[(slot * NC + c) * 64 + lane] = t.c[c];
+            es[(slot * NC + c) * 64 + lane] = e[c];
+        }
+    }
+    static __device__ __forceinline__ void ld(const T* vs, const double* es, int slot, int lane, J& t, double* e) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            t.c[c] = vs[(slot * NC + c) * 64 + lane];
+            e[c] = es[(slot * NC + c) * 64 + lane];
+        }
+    }
+
+    // value + error bound of program words [pc, end) at (x, y)
+    static __device__ int run(const int32_t* ops, int64_t pc, int64_t end, double x, double y, J& acc,
+                              double* ea, T* vs, double* es, int lane) {
+        int d = 0;
+        if (pc >= end) return RUN_BAD;
+        for (;;) {
+            const uint32_t w = rd_word(ops + pc);
+            const uint32_t op = w & 0xffu;
+            double imm = 0.0;
+            int64_t npc = pc + 1;
+            if (op_has_imm(op)) {
+                if (pc + 3 > end) return RUN_BAD;
+                imm = rd_imm(ops + pc + 1);
+                npc = pc + 3;
+            }
+            double A[NC], B[NC], R[NC];
+            switch (op) {
+                case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I: {
+                    if (d > 0 && d < MAXD) st(vs, es, d - 1, lane, acc, ea);
+                    if (op == PDOP_PUSH_X) O::set_var(acc, x, 0);
+                    else if (op == PDOP_PUSH_Y) O::set_var(acc, y, 1);
+                    else if (op == PDOP_PUSH_C) O::set_const(acc, from_real<T>(imm));
+                    else {
+                        if constexpr (Real<T>::cplx_pass) O::set_const(acc, cplx{0.0, 1.0});
+                        else return RUN_UNSUPPORTED;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) ea[i] = 0.0;
+                    if (op == PDOP_PUSH_C) ea[0] = fabs(imm);
+                    ++d;
+                    break;
+                }
+                case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB:
+                case PDOP_MUL: case PDOP_DIV: case PDOP_RDIV: {
+                    if (d >= 2 && d <= MAXD) {
+                        J lhs;
+                        double el[NC];
+                        ld(vs, es, d - 2, lane, lhs, el);
+                        if (op == PDOP_ADD || op == PDOP_SUB || op == PDOP_RSUB) {
+                            Interp<T, K, MAXD>::binop(op, lhs, acc);
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) ea[i] += el[i];
+                            E::add_abs(acc.c, ea);
+                        } else if (op == PDOP_MUL) {
+                            // |a| (*) (E_t + |t|) + E_a (*) |t|
+                            E::absv(lhs.c, A);
+                            E::absv(acc.c, B);
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) R[i] = ea[i] + B[i];
+                            E::mul(A, R, R);
+                            E::mul(el, B, A);
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) ea[i] = R[i] + A[i];
+                            O::mul(lhs, acc);
+                        } else {
+                            // DIV: t = a / t (num a, den t);  RDIV: t = t / a (num t, den a)
+                            const bool dv = op == PDOP_DIV;
+                            E::absv(dv ? acc.c : lhs.c, B);            // |den|
+                            double en[NC];
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) {
+                                en[i] = dv ? el[i] : ea[i];            // E_num
+                                A[i] = dv ? ea[i] : el[i];             // E_den
+                            }
+                            Interp<T, K, MAXD>::binop(op, lhs, acc);
+                            E::absv(acc.c, R);
+                            E::mul(R, A, A);
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) A[i] += en[i];
+                            E::absdiv(A, B, ea);
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) ea[i] += R[i];
+                        }
+                    }
+                    --d;
+                    break;
+                }
+                case PDOP_ADDC:
+                    acc.c[0] = acc.c[0] + from_real<T>(imm);
+                    ea[0] += fabs(imm) + mag(acc.c[0]);
+                    break;
+                case PDOP_MULC:
+                    O::scale(acc, from_real<T>(imm));
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) ea[i] = ea[i] * fabs(imm) + mag(acc.c[i]);
+                    break;
+                case PDOP_RDIVC: {
+                    E::absv(acc.c, B);
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) A[i] = ea[i];
+                    O::rdivc(acc, from_real<T>(imm));
+                    E::absv(acc.c, R);
+                    E::mul(R, A, A);
+                    A[0] += fabs(imm);
+                    E::absdiv(A, B, ea);
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) ea[i] += R[i];
+                    break;
+                }
+                case PDOP_NEG:
+                    O::scale(acc, from_real<T>(-1.0));
+                    break;
+                case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: {
+                    const bool isx = (op == PDOP_ADD_X || op == PDOP_SUB_X);
+                    const double sg = (op == PDOP_ADD_X || op == PDOP_ADD_Y) ? 1.0 : -1.0;
+                    acc.c[0] = acc.c[0] + from_real<T>(sg * (isx ? x : y));
+                    const int idx = isx ? ji(1, 0) : ji(0, 1);
+                    acc.c[idx] = acc.c[idx] + from_real<T>(sg);
+                    ea[0] += mag(acc.c[0]);
+                    break;
+                }
+                case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: {
+                    const int axis = (op == PDOP_MUL_X || op == PDOP_DIV_X) ? 0 : 1;
+                    const double v = axis == 0 ? x : y;
+                    if (op == PDOP_MUL_X || op == PDOP_MUL_Y) {
+                        O::mul_var(acc, v, axis);
+                        // E (*) (|v| + d_axis), in place in decreasing degree
+#pragma unroll
+                        for (int dd = K; dd >= 0; --dd)
+#pragma unroll
+                            for (int j = 0; j <= dd; ++j) {
+                                const int i = dd - j;
+                                double s = ea[ji(i, j)] * fabs(v);
+                                if (axis == 0 && i > 0) s += ea[ji(i - 1, j)];
+                                if (axis == 1 && j > 0) s += ea[ji(i, j - 1)];
+                                ea[ji(i, j)] = s;
+                            }
+                    } else {
+                        O::div_var(acc, v, axis);
+                        // absdiv(E, |v| + d_axis), in place in increasing degree
+                        const double inv = 1.0 / fabs(v);
+#pragma unroll
+                        for (int dd = 0; dd <= K; ++dd)
+#pragma unroll
+                            for (int j = 0; j <= dd; ++j) {
+                                const int i = dd - j;
+                                double s = ea[ji(i, j)];
+                                if (axis == 0 && i > 0) s += ea[ji(i - 1, j)];
+                                if (axis == 1 && j > 0) s += ea[ji(i, j - 1)];
+                                ea[ji(i, j)] = s * inv;
+                            }
+                    }
+                    E::add_abs(acc.c, ea);
+                    break;
+                }
+                case PDOP_POWN: {
+                    // b^n as n-1 products by b: E' = P (*) (E_b + |b|) + E (*) |b|, P >= |b^k|
+                    const int n = (int)((w >> 8) & 0xffu);
+                    double P[NC], eb[NC];
+                    E::absv(acc.c, B);
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) {
+                        P[i] = B[i];
+                        eb[i] = ea[i];
+                        R[i] = ea[i] + B[i];
+                    }
+                    for (int k = 1; k < n; ++k) {
+                        E::mul(P, R, A);
+                        E::mul(ea, B, ea);
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) ea[i] += A[i];
+                        E::mul(P, B, P);
+                    }
+                    (void)eb;
+                    O::pown(acc, n);
+                    break;
+                }
+                case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: {
+                    T f[K + 2];
+                    outer_coefs<T, K>(op, acc.c[0], imm, f);
+                    double G[K + 1], Fa[K + 1];
+#pragma unroll
+                    for (int k = 0; k <= K; ++k) {
+                        G[k] = (k + 1) * mag(f[k + 1]);
+                        Fa[k] = mag(f[k]);
+                    }
+                    E::absv(acc.c, A);
+                    Horner<double, K, 0>::run(A, G, B);     // G1 = sum (m+1)|f_(m+1)| |h|^m
+                    Horner<double, K, 0>::run(A, Fa, R);    // sum |f_k| |h|^k
+                    E::mul(B, ea, ea);
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) ea[i] += R[i];
+                    if (op == PDOP_POW) O::powa(acc, imm);
+                    else if (op == PDOP_SQRT) O::sqrtj(acc);
+                    else if (op == PDOP_EXP) O::expj(acc);
+                    else O::logj(acc);
+                    break;
+                }
+                case PDOP_ABS: absj<K>(acc); break;
+                default: return RUN_UNSUPPORTED;
+            }
+            if (npc >= end) break;
+            pc = npc;
+        }
+        return d == 1 ? RUN_OK : RUN_BAD;
+    }
+};
+
+// First-order rounding-noise bound of the residual at one point.
+template <int PROB, class T> __device__ __forceinline__ double residual_noise(const T* u, const double* e,
+                                                                              double x, const double* kc,
+                                                                              double S) {
+    constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    double up[nc(K)];
+#pragma unroll
+    for (int i = 0; i < nc(K); ++i) up[i] = mag(u[i]) + kNoiseGamma * e[i];
+    double S2;
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) S2 = FFEpi<double, true>::eval(up, x);
+    else S2 = kerr_epilogue<double>(up, kc).scale;
+    return (S2 - S) * (kEps / kNoiseGamma) + kEps * S;
+}
+
+// Persistent over a tier-2 list (entries cand | ESC_* << 48 written by validate_kernel).
+template <int PROB, class T, int MAXD>
+__global__ __launch_bounds__(64, 2) void tier2_kernel(KernelArgs a) {
+    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
+    constexpr int NC = nc(K);
+    using I = ErrInterp<T, K, MAXD>;
+    using J = typename I::J;
+    const int lane = threadIdx.x & 63;
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+    T* vs = reinterpret_cast<T*>(pd_lds);
+    double* es = reinterpret_cast<double*>(pd_lds + (size_t)(MAXD - 1) * NC * 64 * sizeof(T));
+    int64_t nwork = (int64_t)(*a.list_count);
+    if (nwork > a.list_capacity) nwork = a.list_capacity;
+    for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+        const int64_t entry = a.list[wi];
+        const int64_t cand = entry & PD_ESC_CAND_MASK;
+        const uint32_t flags = (uint32_t)(entry >> PD_ESC_SHIFT);
+        const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
+        const uint32_t hdr = rd_word(a.ops + beg);
+        const int depth = (int)((hdr >> 8) & 0xffu);
+        if (depth > MAXD) {
+            if (lane == 0 && a.defer_list) list_append(a.defer_list, a.defer_count, a.list_capacity, entry);
+            continue;
+        }
+        // ---- point stage (only if it failed tier 1)
+        bool point_reject = false;
+        bool grad_nz = false;
+        if (flags & ESC_POINT) {
+            const bool active = lane < a.n_ref;
+            const int l = active ? lane : 0;
+            const double x = l == 0 ? a.ref_x[0] : (l == 1 ? a.ref_x[1] : (l == 2 ? a.ref_x[2] : a.ref_x[3]));
+            const double y = l == 0 ? a.ref_y[0] : (l == 1 ? a.ref_y[1] : (l == 2 ? a.ref_y[2] : a.ref_y[3]));
+            J u;
+            double e[NC];
+            const int rc = I::run(a.ops, beg + 1, end, x, y, u, e, vs, es, lane);
+            bool real_fail = rc != RUN_OK;
+            if (rc == RUN_OK) {
+                const double* kc = a.kc ? a.kc + 4 * l : nullptr;
+                PointResult r;
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x);
+                else r = kerr_epilogue<T>(u.c, kc);
+                bool fails;
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) fails = !(scaled(r.res_abs, r.scale) <= a.prm.tau_point);
+                else fails = !(r.res_abs < a.prm.kerr_abs_tol);
+                if (!r.finite) real_fail = true;
+                else if (fails) real_fail = r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale);
+            }
+            point_reject = __any(active && real_fail);
+            if (point_reject) continue;     // confirmed: pass 1's REJECT_POINT stands
+        }
+        // ---- grid stage
+        int nbad_out = -1, nb1 = 0, nb2 = 0, nfin = 0, nnonfin = 0;
+        double qmax = 0.0;
+        const bool eval_grid = !(flags & ESC_GRID_EVAL) || (flags & ESC_GRID_FAIL);
+        if (eval_grid) {
+            const int per_row = a.ny >> 6;
+            const int nchunks = a.nx * per_row;
+            for (int ch = 0; ch < nchunks; ++ch) {
+                const int row = ch / per_row, sl = ch - row * per_row;
+                const int p = a.n_ref + row * a.ny + sl * 64 + lane;
+                const double x = *(const __attribute__((address_space(4))) double*)(a.gx + row);
+                const double y = a.gy[sl * 64 + lane];
+                J u;
+                double e[NC];
+                const int rc = I::run(a.ops, beg + 1, end, x, y, u, e, vs, es, lane);
+                if (rc != RUN_OK) { ++nnonfin; continue; }
+                const double* kc = a.kc ? a.kc + 4 * p : nullptr;
+                PointResult r;
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x);
+                else r = kerr_epilogue<T>(u.c, kc);
+                if (!r.finite) { ++nnonfin; continue; }
+                ++nfin;
+                const double qv = scaled(r.res_abs, r.scale);
+                qmax = fmax(qmax, qv);
+                if (!r.grad_zero) grad_nz = true;
+                if (qv > a.prm.tau_grid) {
+                    ++nb1;
+                    if (r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale)) ++nb2;
+                }
+            }
+            nb1 = wave_sum(nb1);
+            nb2 = wave_sum(nb2);
+            nfin = wave_sum(nfin);
+            nnonfin = wave_sum(nnonfin);
+            qmax = wave_max(qmax);
+            nbad_out = nb1 <= a.prm.max_bad ? nb1 : nb2;
+        }
+        const bool any_grad = __any(grad_nz) || (flags & ESC_ANY_GRAD);
+        if (lane == 0) {
+            const bool has_fin = eval_grid ? nfin > 0 : (flags & ESC_NFIN) != 0;
+            const bool structural = (PROB != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);
+            int cls;
+            if (!any_grad && has_fin && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+            else if (nbad_out > a.prm.max_bad) cls = PDEVAL_CLS_REJECT_GRID;
+            else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic && (hdr & PDEVAL_FLAG_NONSMOOTH2D))
+                cls = PDEVAL_CLS_REJECT_SYMBOLIC;
+            else cls = PDEVAL_CLS_ACCEPT;
+            if (a.out.status) a.out.status[cand] = (uint8_t)cls;
+            if (eval_grid) {
+                if (a.out.n_bad) a.out.n_bad[cand] = nbad_out;
+                if (!(flags & ESC_GRID_EVAL)) {
+                    if (a.out.q_grid) a.out.q_grid[cand] = qmax;
+                    if (a.out.n_nonfinite) a.out.n_nonfinite[cand] = nnonfin;
+                }
+            }
+            if (a.out.verdict_bits && cls == PDEVAL_CLS_ACCEPT)
+                atomicOr((uint32_t*)a.out.verdict_bits + (cand >> 5), 1u << (cand & 31));
+        }
+    }
+}
+
+}  // namespace pd

@@ -22,13 +22,17 @@ EXPORTS = (
     'pdeval_create', 'pdeval_destroy', 'pdeval_last_error', 'pdeval_n_ref_points',
     'pdeval_n_points', 'pdeval_default_params', 'pdeval_validate_batch',
     'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
+    'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts',
 )
+LIST_NAMES = ('defer_stack4', 'complex', 'defer_stack8', 'tier2', 'tier2_deep', 'tier2_complex')
+N_PASSES = 7
 
 
 class Params(C.Structure):
     _fields_ = [('tau_point', C.c_double), ('tau_grid', C.c_double),
                 ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32),
-                ('strict_symbolic', C.c_int32), ('reserved', C.c_int32)]
+                ('strict_symbolic', C.c_int32), ('reserved', C.c_int32),
+                ('noise_kappa', C.c_double)]
 
 
 class Outputs(C.Structure):
@@ -68,6 +72,9 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_program_flops.argtypes = [C.c_int, vp, i64]
     lib.pdeval_program_flops.restype = dbl
     lib.pdeval_version.restype = C.c_char_p
+    lib.pdeval_set_timing.argtypes = [vp, C.c_int]
+    lib.pdeval_pass_times.argtypes = [vp, vp, C.c_int, vp]
+    lib.pdeval_pass_counts.argtypes = [vp, vp, C.c_int]
     for name in EXPORTS:
         getattr(lib, name)   # every symbol of the header must resolve
     if path is None:
@@ -147,6 +154,22 @@ class Context:
         res['fingerprint'] = res['fingerprint'].reshape(n, FP_N)
         res['verdict'] = np.unpackbits(res['verdict_bits'], bitorder='little')[:n].astype(bool)
         return res
+
+    def set_timing(self, enable: bool = True):
+        _check(self.h, self.lib.pdeval_set_timing(self.h, int(enable)))
+
+    def pass_times(self):
+        """{pass name: ms} of the most recent validate_device call (timing enabled)."""
+        ms = (C.c_float * N_PASSES)()
+        names = (C.c_char_p * N_PASSES)()
+        _check(self.h, self.lib.pdeval_pass_times(self.h, ms, N_PASSES, names))
+        return {names[k].decode(): float(ms[k]) for k in range(N_PASSES)}
+
+    def pass_counts(self):
+        """{work list: entries} of the most recent call (synchronizes)."""
+        c = (C.c_int64 * len(LIST_NAMES))()
+        _check(self.h, self.lib.pdeval_pass_counts(self.h, c, len(LIST_NAMES)))
+        return {k: int(c[i]) for i, k in enumerate(LIST_NAMES)}
 
     def validate_device(self, d_ops: int, n_words: int, d_offsets: int, n: int, d_out: Outputs,
                         params: Optional[Params] = None, stream: int = 0, zero_bits: bool = True):

@@ -27,3 +27,9 @@ def stream(name, with_index=False):
 
 FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl')
 KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl')
+
+
+def exact_rows(name='ff_d4_exact_det.jsonl'):
+    """Exact-arithmetic ground truth (gen_exact_det.py): det_zero = true solution."""
+    with open(os.path.join(GOLDEN, 'exact', name)) as f:
+        return [json.loads(l) for l in f]

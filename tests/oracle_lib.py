@@ -23,18 +23,21 @@ def load():
         _lib.oracle_validate.argtypes = [C.c_int, vp, vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp,
                                          vp, C.c_int64, C.c_int64]
         _lib.oracle_jet.argtypes = [C.c_int, vp, C.c_int64, C.c_double, C.c_double, C.c_int, vp, vp]
+        _lib.oracle_point.argtypes = [C.c_int, vp, C.c_int64, C.c_double, C.c_double, C.c_int, vp]
     return _lib
 
 
 class _Params(C.Structure):
     _fields_ = [('tau_point', C.c_double), ('tau_grid', C.c_double),
                 ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32),
-                ('strict_symbolic', C.c_int32), ('reserved', C.c_int32)]
+                ('strict_symbolic', C.c_int32), ('reserved', C.c_int32),
+                ('noise_kappa', C.c_double)]
 
 
 def params(tau_point=1e-10, tau_grid=1e-7, kerr_abs_tol=1e-10, full_grid=1, max_bad=0,
-           strict_symbolic=1):
-    return _Params(tau_point, tau_grid, kerr_abs_tol, full_grid, max_bad, strict_symbolic, 0)
+           strict_symbolic=1, noise_kappa=16.0):
+    return _Params(tau_point, tau_grid, kerr_abs_tol, full_grid, max_bad, strict_symbolic, 0,
+                   noise_kappa)
 
 
 def validate(problem_id, ops, offsets, prm=None, first=0, count=-1, n_ref=None):
@@ -66,3 +69,14 @@ def jet(problem_id, words, x, y, cplx=False):
     if rc:
         raise ValueError(f'oracle_jet rc={rc}')
     return re + 1j * im if cplx else re
+
+
+def point(problem_id, words, x, y, cplx=False):
+    """(|residual|, S, noise bound, finite) at one point, with the tier-2 noise bound."""
+    lib = load()
+    w = np.ascontiguousarray(words, dtype=np.int32)
+    out = np.zeros(4)
+    rc = lib.oracle_point(problem_id, w.ctypes.data, w.size, x, y, int(cplx), out.ctypes.data)
+    if rc:
+        raise ValueError(f'oracle_point rc={rc}')
+    return out

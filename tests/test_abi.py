@@ -41,7 +41,7 @@ def test_opcodes_match_header():
 
 def test_params_struct_layout():
     import ctypes as C
-    assert C.sizeof(_lib.Params) == 40
+    assert C.sizeof(_lib.Params) == 48
     assert C.sizeof(_lib.Outputs) == 64
     p = _lib.default_params(0)
     assert p.tau_point == 1e-10 and p.kerr_abs_tol == 1e-10 and p.full_grid == 1

@@ -45,8 +45,10 @@ def _cmp_device_oracle(ctx, pd_, strings):
     ora = O.validate(pd_.problem_id, ops, off)
     assert np.array_equal(dev['status'], ora['status']), \
         [(s, int(a), int(b)) for s, a, b in zip(strings, dev['status'], ora['status']) if a != b][:10]
-    assert np.array_equal(dev['n_bad'], ora['n_bad'])
-    assert np.array_equal(dev['n_nonfinite'], ora['n_nonfinite'])
+    for k in ('n_bad', 'n_nonfinite'):
+        bad = np.flatnonzero(dev[k] != ora[k])
+        assert not bad.size, (k, [(strings[i], int(dev['status'][i]), int(dev[k][i]), int(ora[k][i]))
+                                  for i in bad[:10]])
     check_residuals(dev, ora, strings)
     return dev, ora
 
@@ -107,3 +109,28 @@ def test_plugin_api_reasons():
     # the per-candidate contract of problems/__init__.py:52
     assert prob.validator.validate(us[0], check_regularity=False) == got[0]
     assert all(prob.validator.validate_known_solutions().values())
+
+
+def test_ff_tier2_exact_ground_truth(ff_ctx):
+    """Tier 2 on the device: true solutions (exact det = 0) accepted, the rest rejected, and
+    the classes equal the oracle's."""
+    pd_ = P.force_free()
+    rows = G.exact_rows()
+    dev, _ = _cmp_device_oracle(ff_ctx, pd_, [r['expr'] for r in rows])
+    wrong = [(r['expr'], int(s)) for r, s in zip(rows, dev['status']) if (s in (0, 7)) != r['det_zero']]
+    assert not wrong, wrong[:10]
+
+
+def test_ff_early_exit_same_verdicts(ff_ctx):
+    """The reference's control flow (stop after the point stage) gives the same verdicts."""
+    from pdeval._lib import default_params
+    pd_ = P.force_free()
+    rows = G.exact_rows() + G.decided(G.ref_rows(*G.FF_REF))
+    ops, off, _ = P.compile_strings(pd_, [r['expr'] for r in rows])
+    full = ff_ctx.validate(ops, off)
+    prm = default_params(0)
+    prm.full_grid = 0
+    early = ff_ctx.validate(ops, off, prm)
+    assert np.array_equal(full['verdict'], early['verdict'])
+    ora = O.validate(0, ops, off, O.params(full_grid=0))
+    assert np.array_equal(early['status'], ora['status'])
