@@ -163,12 +163,12 @@ int pdeval_validate_device(pdeval_ctx* ctx, const int32_t* d_ops, int64_t n_word
  * the launch stream (passes a problem does not run take 0 ms).  pdeval_pass_times waits for
  * the last event of the most recent call and writes min(max_passes, PDEVAL_N_PASSES)
  * durations in ms (and, if names != NULL, a static name per pass).                       */
-#define PDEVAL_N_PASSES 7
+#define PDEVAL_N_PASSES 9
 int pdeval_set_timing(pdeval_ctx* ctx, int enable);
 int pdeval_pass_times(pdeval_ctx* ctx, float* ms, int max_passes, const char** names);
-/* Work-list sizes of the most recent call (synchronizes the device): [0] deferred to pass 2,
- * [1] complex pass, [2] deferred to pass 3, [3] tier-2 entries, [4] tier-2 deep, [5] tier-2
- * complex.                                                                                */
+/* Work-list sizes of the most recent call (synchronizes the device): [0] deferred to the
+ * stack-3 pass, [1] complex passes, [2] deferred to the stack-8 pass, [3] tier-2 entries,
+ * [4] tier-2 stack 3, [5] tier-2 complex, [6] complex stack 8, [7] tier-2 stack 8.        */
 int pdeval_pass_counts(pdeval_ctx* ctx, int64_t* counts, int max_counts);
 
 /* Host-side program analysis (no GPU): required stack depth, or < 0 if malformed.      */

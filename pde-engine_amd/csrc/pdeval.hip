@@ -21,6 +21,19 @@ using namespace pd;
 
 #define PD_VERSION "pdeval 0.1 gfx950"
 
+// Work lists between the passes of one call (pdeval_pass_counts reports their sizes).
+enum {
+    L_DEFER = 0,      // pass 1 -> pass 2: real, stack 3
+    L_CPLX = 1,       // pass 1 -> complex passes: not real at the reference point
+    L_DEFER2 = 2,     // pass 2 -> pass 3: real, stack 4..8
+    L_ESC = 3,        // tier-1 failures of the real passes -> tier 2
+    L_ESC_DEEP = 4,   // tier 2 stack 2 -> tier 2 stack 3
+    L_ESC_C = 5,      // tier-1 failures of the complex passes -> complex tier 2
+    L_CPLX_DEEP = 6,  // complex stack 2 -> complex stack 8
+    L_ESC_DEEP2 = 7,  // tier 2 stack 3 -> tier 2 stack 8
+    PD_N_LISTS = 8
+};
+
 struct pdeval_ctx {
     int device = 0;
     int problem = 0;
@@ -34,13 +47,9 @@ struct pdeval_ctx {
     double* d_kc = nullptr;
     // scratch: work lists and their counters
     int64_t cap = 0;
-    int64_t* d_defer = nullptr;   // pass 1 -> pass 2 (stack 3..4)
-    int64_t* d_defer2 = nullptr;  // pass 2 -> pass 3 (stack 5..8)
-    int64_t* d_cplx = nullptr;
-    int64_t* d_esc = nullptr;       // tier-2 escalations, real passes
-    int64_t* d_esc_deep = nullptr;  // tier-2 entries deeper than the first tier-2 variant
-    int64_t* d_esc_c = nullptr;     // tier-2 escalations of the complex pass
-    int32_t* d_counts = nullptr;  // [0] defer, [1] cplx, [2] defer2, [3] esc, [4] esc_deep, [5] esc_c
+    // device work lists (capacity cap each) and their counters d_counts[L_*]
+    int64_t* d_list[PD_N_LISTS] = {};
+    int32_t* d_counts = nullptr;
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -56,8 +65,8 @@ struct pdeval_ctx {
 };
 
 static const char* const kPassNames[PDEVAL_N_PASSES] = {
-    "pass1_stack2", "pass2_stack4", "pass3_stack8", "pass4_complex",
-    "tier2_stack2", "tier2_stack8", "tier2_complex"};
+    "pass1_stack2", "pass2_stack3", "pass3_stack8", "complex_stack2", "complex_stack8",
+    "tier2_stack2", "tier2_stack3", "tier2_stack8", "tier2_complex"};
 
 static thread_local std::string g_err;
 
@@ -184,7 +193,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
         if ((e = hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
             return fail("hipMemcpy", e);
     }
-    if ((e = hipMalloc(&c->d_counts, 8 * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc(&c->d_counts, PD_N_LISTS * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
     *out = c;
     return PDEVAL_OK;
 }
@@ -193,8 +202,9 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (!c) return PDEVAL_ERR_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc, (void*)c->d_defer, (void*)c->d_defer2, (void*)c->d_cplx,
-                    (void*)c->d_esc, (void*)c->d_esc_deep, (void*)c->d_esc_c,
+    for (int64_t* l : c->d_list)
+        if (l) (void)hipFree(l);
+    for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) hipFree(p);
     for (hipEvent_t& e : c->ev)
@@ -305,18 +315,13 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
 // ---------------------------------------------------------------------------- launches
 static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (n <= c->cap) return PDEVAL_OK;
-    for (int64_t** p : {&c->d_defer, &c->d_defer2, &c->d_cplx, &c->d_esc, &c->d_esc_deep, &c->d_esc_c}) {
-        if (*p) (void)hipFree(*p);
-        *p = nullptr;
+    for (int64_t*& l : c->d_list) {
+        if (l) (void)hipFree(l);
+        l = nullptr;
     }
     c->cap = 0;
     const int64_t cap = n < 1024 ? 1024 : n;
-    HIPCHK(c, hipMalloc(&c->d_defer, cap * sizeof(int64_t)));
-    HIPCHK(c, hipMalloc(&c->d_defer2, cap * sizeof(int64_t)));
-    HIPCHK(c, hipMalloc(&c->d_cplx, cap * sizeof(int64_t)));
-    HIPCHK(c, hipMalloc(&c->d_esc, cap * sizeof(int64_t)));
-    HIPCHK(c, hipMalloc(&c->d_esc_deep, cap * sizeof(int64_t)));
-    HIPCHK(c, hipMalloc(&c->d_esc_c, cap * sizeof(int64_t)));
+    for (int64_t*& l : c->d_list) HIPCHK(c, hipMalloc(&l, cap * sizeof(int64_t)));
     c->cap = cap;
     return PDEVAL_OK;
 }
@@ -356,95 +361,89 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     for (int f = 0; f < PDEVAL_FP_N; ++f) a.fp_pts[f] = c->fp_pts[f];
     a.prm = prm;
     a.out = o;
-    a.defer_list = c->d_defer;
-    a.defer_count = c->d_counts;
-    a.cplx_list = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? c->d_cplx : nullptr;
-    a.cplx_count = c->d_counts + 1;
     a.list_capacity = c->cap;
-    a.esc_list = c->d_esc;
-    a.esc_count = c->d_counts + 3;
-    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, 8 * sizeof(int32_t), s));
-    constexpr int WPB = 4;  // waves (candidates) per 256-thread block
-    const int64_t blocks = (n + WPB - 1) / WPB;
-    // pass 1: programs whose stack fits 2 jets (>92 % of force-free depth 4), one wave per
-    // candidate; deeper programs are appended to a device list
-    a.defer_list = c->d_defer;
-    a.defer_count = c->d_counts + 0;
+    int32_t* const cnt = c->d_counts;
+    HIPCHK(c, hipMemsetAsync(cnt, 0, PD_N_LISTS * sizeof(int32_t), s));
     constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    constexpr bool FF = PROB == PDEVAL_PROBLEM_FORCE_FREE;
+    constexpr int WPB = 4;  // waves (candidates) per 256-thread block of pass 1
+    const int64_t blocks = (n + WPB - 1) / WPB;
+    // one list-driven pass: persistent one-wave blocks over list `in`, programs deeper than
+    // the variant's stack appended to `out`, tier-1 failures to `esc`
+    auto follow = [&](int in, int out, int esc) {
+        KernelArgs b = a;
+        b.list = c->d_list[in];
+        b.list_count = cnt + in;
+        b.defer_list = out >= 0 ? c->d_list[out] : nullptr;
+        b.defer_count = out >= 0 ? cnt + out : nullptr;
+        b.cplx_list = FF ? c->d_list[L_CPLX] : nullptr;   // real passes: not real at p* -> complex
+        b.cplx_count = cnt + L_CPLX;
+        b.esc_list = c->d_list[esc];
+        b.esc_count = cnt + esc;
+        return b;
+    };
+    const unsigned pgrid = (unsigned)std::min<int64_t>(4 * blocks, 8192);
+    // pass 1: programs whose stack fits 2 jets (92 % of force-free depth 4), one wave per
+    // candidate; deeper programs and complex-valued candidates go to device lists
+    a.defer_list = c->d_list[L_DEFER];
+    a.defer_count = cnt + L_DEFER;
+    a.cplx_list = FF ? c->d_list[L_CPLX] : nullptr;
+    a.cplx_count = cnt + L_CPLX;
+    a.esc_list = c->d_list[L_ESC];
+    a.esc_count = cnt + L_ESC;
     mark(0);
     hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256),
                        (stack_lds<double, K, 2>(4)), s, a);
     HIPCHK(c, hipGetLastError());
-    // pass 2: deferred programs with stack 3..4 (register stack), persistent over list 1;
-    // deeper ones go on to list 2
-    KernelArgs b = a;
-    b.list = c->d_defer;
-    b.list_count = c->d_counts + 0;
-    b.defer_list = c->d_defer2;
-    b.defer_count = c->d_counts + 2;
-    const int64_t pblocks = std::min<int64_t>(blocks, 2048);
-    // follow-up passes: one wave per block (their LDS stacks are deeper)
+    // pass 2: stack 3 (7 % of force-free depth 4; 2 LDS slots keep 10 waves per CU)
     mark(1);
-    hipLaunchKernelGGL((validate_kernel<PROB, double, 4, true>), dim3((unsigned)(4 * pblocks)), dim3(64),
-                       (stack_lds<double, K, 4>(1)), s, b);
+    hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3(pgrid), dim3(64),
+                       (stack_lds<double, K, 3>(1)), s, follow(L_DEFER, L_DEFER2, L_ESC));
     HIPCHK(c, hipGetLastError());
-    // pass 3: stack 5..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
-    KernelArgs b2 = a;
-    b2.list = c->d_defer2;
-    b2.list_count = c->d_counts + 2;
-    b2.defer_list = nullptr;
+    // pass 3: stack 4..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
     mark(2);
     hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
                        dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
-                       (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, b2);
+                       (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
     HIPCHK(c, hipGetLastError());
-    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-        // pass 4: candidates not real at the reference point, in complex arithmetic
-        KernelArgs x = a;
-        x.list = c->d_cplx;
-        x.list_count = c->d_counts + 1;
-        x.cplx_list = nullptr;
-        x.defer_list = nullptr;
-        x.esc_list = c->d_esc_c;
-        x.esc_count = c->d_counts + 5;
-        const int64_t cblocks = std::min<int64_t>(blocks, 2048);
+    if constexpr (FF) {
+        // complex passes: candidates not real at the reference point, in complex arithmetic
+        // (SymPy evaluates the point exactly, in the complex field: validator.py:363-402)
         mark(3);
-        hipLaunchKernelGGL((validate_kernel<PROB, cplx, 4, true>), dim3((unsigned)(4 * cblocks)),
-                           dim3(64), (stack_lds<cplx, K, 4>(1)), s, x);
+        hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3(pgrid), dim3(64),
+                           (stack_lds<cplx, K, 2>(1)), s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C));
+        HIPCHK(c, hipGetLastError());
+        mark(4);
+        hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),
+                           dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
+                           (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
         HIPCHK(c, hipGetLastError());
     } else {
         mark(3);
+        mark(4);
     }
-    // tier 2 (pdeval_tier2.h): re-decide every tier-1 failure with error bounds.  Stack <= 2
-    // first; deeper programs go on to the MAXD = 8 variant; complex candidates separately.
-    KernelArgs t = a;
-    t.list = c->d_esc;
-    t.list_count = c->d_counts + 3;
-    t.defer_list = c->d_esc_deep;
-    t.defer_count = c->d_counts + 4;
-    mark(4);
+    // tier 2 (pdeval_tier2.h): re-decide every tier-1 failure with error bounds, by stack depth
+    KernelArgs t = follow(L_ESC, L_ESC_DEEP, L_ESC);
+    mark(5);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, 2>), dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(64),
                        (tier2_lds<double, K, 2>()), s, t);
     HIPCHK(c, hipGetLastError());
-    KernelArgs t2 = a;
-    t2.list = c->d_esc_deep;
-    t2.list_count = c->d_counts + 4;
-    t2.defer_list = nullptr;
-    mark(5);
-    hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
-                       dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, t2);
+    mark(6);
+    hipLaunchKernelGGL((tier2_kernel<PROB, double, 3>), dim3((unsigned)std::min<int64_t>(n, 4096)), dim3(64),
+                       (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
     HIPCHK(c, hipGetLastError());
-    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-        KernelArgs tc = a;
-        tc.list = c->d_esc_c;
-        tc.list_count = c->d_counts + 5;
-        tc.defer_list = nullptr;
-        mark(6);
+    mark(7);
+    hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
+                       dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, follow(L_ESC_DEEP2, -1, L_ESC));
+    HIPCHK(c, hipGetLastError());
+    if constexpr (FF) {
+        // (complex programs deeper than 4 keep their tier-1 class: 161 KiB of LDS would not fit)
+        mark(8);
         hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4>), dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(64),
-                           (tier2_lds<cplx, K, 4>()), s, tc);
+                           (tier2_lds<cplx, K, 4>()), s, follow(L_ESC_C, -1, L_ESC_C));
         HIPCHK(c, hipGetLastError());
     } else {
-        mark(6);
+        mark(8);
     }
     mark(PDEVAL_N_PASSES);
     c->ev_recorded = c->timing ? 1 : 0;
@@ -583,10 +582,9 @@ extern "C" int pdeval_pass_times(pdeval_ctx* c, float* ms, int max_passes, const
 extern "C" int pdeval_pass_counts(pdeval_ctx* c, int64_t* counts, int max_counts) {
     if (!c || !counts || max_counts < 0) return PDEVAL_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    int32_t h[8] = {0};
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int32_t h[PD_N_LISTS] = {0};
     HIPCHK(c, hipDeviceSynchronize());
     HIPCHK(c, hipMemcpy(h, c->d_counts, sizeof(h), hipMemcpyDeviceToHost));
-    for (int k = 0; k < max_counts && k < 8; ++k) counts[k] = h[k];
+    for (int k = 0; k < max_counts && k < PD_N_LISTS; ++k) counts[k] = h[k];
     return PDEVAL_OK;
 }

@@ -24,8 +24,9 @@ EXPORTS = (
     'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
     'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts',
 )
-LIST_NAMES = ('defer_stack4', 'complex', 'defer_stack8', 'tier2', 'tier2_deep', 'tier2_complex')
-N_PASSES = 7
+LIST_NAMES = ('defer_stack3', 'complex', 'defer_stack8', 'tier2', 'tier2_stack3', 'tier2_complex',
+              'complex_stack8', 'tier2_stack8')
+N_PASSES = 9
 
 
 class Params(C.Structure):
