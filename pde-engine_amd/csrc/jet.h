@@ -76,15 +76,23 @@ PD_HD cplx sqrt_(cplx a) {
     double t = sqrt(0.5 * (m - a.re));
     return {fabs(a.im) / (2.0 * t), copysign(t, a.im)};
 }
-PD_HD double exp_(double a) { return exp(a); }
-PD_HD cplx exp_(cplx a) {
+// The transcendental routines are kept out of line: inlined, their polynomial constants are
+// hoisted out of the interpreter loop by LICM and then spilled to scratch, which costs every
+// candidate; called, they cost only the (rare) EXP / LOG / general-POW opcodes.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PD_TRANS __host__ __device__ __attribute__((noinline))
+#else
+#define PD_TRANS __host__ __device__ inline
+#endif
+PD_TRANS double exp_(double a) { return exp(a); }
+PD_TRANS cplx exp_(cplx a) {
     double e = exp(a.re);
     return {e * cos(a.im), e * sin(a.im)};
 }
-PD_HD double log_(double a) { return log(a); }
-PD_HD cplx log_(cplx a) { return {log(hypot(a.re, a.im)), atan2(a.im, a.re)}; }
-PD_HD double pow_gen(double a, double e) { return pow(a, e); }
-PD_HD cplx pow_gen(cplx a, double e) {
+PD_TRANS double log_(double a) { return log(a); }
+PD_TRANS cplx log_(cplx a) { return {log(hypot(a.re, a.im)), atan2(a.im, a.re)}; }
+PD_TRANS double pow_gen(double a, double e) { return pow(a, e); }
+PD_TRANS cplx pow_gen(cplx a, double e) {
     if (a.re == 0.0 && a.im == 0.0) return {e > 0 ? 0.0 : INFINITY, 0.0};
     cplx l = log_(a);
     return exp_(cplx{l.re * e, l.im * e});

@@ -525,7 +525,7 @@ template <class T, int K, int MAXD> struct Interp {
     }
 
     // Evaluate program words [pc, end) at point (x, y); result jet in T.
-    static __device__ __forceinline__ int run(const int32_t* ops, int64_t pc, int64_t end, double x, double y,
+    static __device__ __forceinline__ int run(const int32_t* ops, int pc, int end, double x, double y,
                                               J& acc, T* stk, int lane) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
@@ -535,7 +535,7 @@ template <class T, int K, int MAXD> struct Interp {
             // immediate and next opcode word are fetched before this op's jet arithmetic, so
             // their scalar-load latency hides under it
             double imm = 0.0;
-            int64_t npc = pc + 1;
+            int npc = pc + 1;
             if (op_has_imm(op)) {
                 if (pc + 3 > end) return RUN_BAD;
                 imm = rd_imm(ops + pc + 1);
@@ -636,12 +636,13 @@ __global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(Kernel
     for (int64_t wi = wave0; wi < nwork; wi = PERSISTENT ? wi + wstride : nwork) {
         const int64_t cand = a.list ? (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]) : wi;
         int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
-        const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words;
+        // programs are addressed relative to their first word with 32-bit offsets
+        const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24);
         if (!in_bounds) beg = end = 0;
-        beg = __builtin_amdgcn_readfirstlane((int)beg);
-        end = __builtin_amdgcn_readfirstlane((int)end);
+        const int32_t* prog = a.ops + beg;
+        const int plen = __builtin_amdgcn_readfirstlane((int)(end - beg));
         // header word: opcode 0, depth in bits 8-15, flags above
-        const uint32_t hdr = in_bounds ? rd_word(a.ops + beg) : 0xffu;
+        const uint32_t hdr = in_bounds ? rd_word(prog) : 0xffu;
         int status = -1;
         if ((hdr & 0xffu) != 0u) status = PDEVAL_CLS_BAD_PROGRAM;
         if constexpr (!Real<T>::cplx_pass) {
@@ -694,7 +695,7 @@ __global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(Kernel
             }
             const int pp = p;
             J u;
-            const int rc = I::run(a.ops, beg + 1, end, x, y, u, stk, lane);
+            const int rc = I::run(prog, 1, plen, x, y, u, stk, lane);
             if (rc == RUN_UNSUPPORTED) { status = PDEVAL_CLS_UNSUPPORTED; break; }
             if (rc == RUN_BAD) { status = PDEVAL_CLS_BAD_PROGRAM; break; }
             PointResult r;

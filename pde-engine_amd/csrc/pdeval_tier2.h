@@ -111,7 +111,7 @@ template <class T, int K, int MAXD> struct ErrInterp {
     }
 
     // value + error bound of program words [pc, end) at (x, y)
-    static __device__ int run(const int32_t* ops, int64_t pc, int64_t end, double x, double y, J& acc,
+    static __device__ int run(const int32_t* ops, int pc, int end, double x, double y, J& acc,
                               double* ea, T* vs, double* es, int lane) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
@@ -119,7 +119,7 @@ template <class T, int K, int MAXD> struct ErrInterp {
             const uint32_t w = rd_word(ops + pc);
             const uint32_t op = w & 0xffu;
             double imm = 0.0;
-            int64_t npc = pc + 1;
+            int npc = pc + 1;
             if (op_has_imm(op)) {
                 if (pc + 3 > end) return RUN_BAD;
                 imm = rd_imm(ops + pc + 1);
@@ -340,7 +340,9 @@ __global__ __launch_bounds__(64, 2) void tier2_kernel(KernelArgs a) {
         const int64_t cand = entry & PD_ESC_CAND_MASK;
         const uint32_t flags = (uint32_t)(entry >> PD_ESC_SHIFT);
         const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
-        const uint32_t hdr = rd_word(a.ops + beg);
+        const int32_t* prog = a.ops + beg;     // bounds were checked by pass 1
+        const int plen = (int)(end - beg);
+        const uint32_t hdr = rd_word(prog);
         const int depth = (int)((hdr >> 8) & 0xffu);
         if (depth > MAXD) {
             if (lane == 0 && a.defer_list) list_append(a.defer_list, a.defer_count, a.list_capacity, entry);
@@ -356,7 +358,7 @@ __global__ __launch_bounds__(64, 2) void tier2_kernel(KernelArgs a) {
             const double y = l == 0 ? a.ref_y[0] : (l == 1 ? a.ref_y[1] : (l == 2 ? a.ref_y[2] : a.ref_y[3]));
             J u;
             double e[NC];
-            const int rc = I::run(a.ops, beg + 1, end, x, y, u, e, vs, es, lane);
+            const int rc = I::run(prog, 1, plen, x, y, u, e, vs, es, lane);
             bool real_fail = rc != RUN_OK;
             if (rc == RUN_OK) {
                 const double* kc = a.kc ? a.kc + 4 * l : nullptr;
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(64, 2) void tier2_kernel(KernelArgs a) {
                 const double y = a.gy[sl * 64 + lane];
                 J u;
                 double e[NC];
-                const int rc = I::run(a.ops, beg + 1, end, x, y, u, e, vs, es, lane);
+                const int rc = I::run(prog, 1, plen, x, y, u, e, vs, es, lane);
                 if (rc != RUN_OK) { ++nnonfin; continue; }
                 const double* kc = a.kc ? a.kc + 4 * p : nullptr;
                 PointResult r;

@@ -19,15 +19,16 @@ EPS = 2.0 ** -52
 
 
 def check_residuals(dev, ora, strings, tau=1e-10):
-    """Residual at the reference point(s).  Point-stage rejects (q > tau): the device value
-    agrees with the oracle's to 1e-10 relative -- or, where the residual itself is the result
-    of cancellation, to the fp64 conditioning limit 64 eps / q (neither side is exact there).
-    Point-stage passes: the residual is rounding noise of an exact zero; both must be noise
-    (q <= tau), which the equal statuses already assert."""
+    """Residual at the reference point(s) of every point-stage reject (class REJECT_POINT):
+    the device value agrees with the oracle's to 1e-10 relative -- or, where the residual
+    itself is the result of cancellation, to the fp64 conditioning limit 64 eps / q (neither
+    side is exact there).  Every other candidate's residual is rounding noise of an exact
+    zero (q <= tau, or |res| within its noise bound: tier 2), which the equal classes already
+    assert."""
     q = np.asarray(ora['q_ref'])
     d, o = dev['res_ref'], ora['res_ref']
     for i in range(len(q)):
-        if not (q[i] > tau) or not np.all(np.isfinite(o[i])):
+        if ora['status'][i] != 1 or not (q[i] > tau) or not np.all(np.isfinite(o[i])):
             continue
         tol = max(REL_TOL, 64 * EPS / q[i]) if dev['res_ref'].shape[1] == 1 else REL_TOL
         err = np.max(np.abs(d[i] - o[i]) / np.maximum(np.abs(o[i]), 1e-300))
