@@ -618,7 +618,13 @@ template <int PROB, class T, int MAXD, bool PERSISTENT>
 #ifndef PD_WAVES_PER_SIMD
 #define PD_WAVES_PER_SIMD 4
 #endif
-__global__ __launch_bounds__(256, PD_WAVES_PER_SIMD) void validate_kernel(KernelArgs a) {
+#ifndef PD_CPLX_WAVES_PER_SIMD
+#define PD_CPLX_WAVES_PER_SIMD 2
+#endif
+// real passes: 128 VGPRs, 4 waves per SIMD; the complex passes need more registers (their
+// jets are twice as wide) and run at 2 waves per SIMD without spilling (12.5 vs 30 ms)
+__global__ __launch_bounds__(256, Real<T>::cplx_pass ? PD_CPLX_WAVES_PER_SIMD : PD_WAVES_PER_SIMD)
+void validate_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
     using I = Interp<T, K, MAXD>;
     using J = typename I::J;

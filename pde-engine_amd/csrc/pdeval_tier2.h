@@ -323,8 +323,11 @@ template <int PROB, class T> __device__ __forceinline__ double residual_noise(co
 }
 
 // Persistent over a tier-2 list (entries cand | ESC_* << 48 written by validate_kernel).
+#ifndef PD_T2_WAVES_PER_SIMD
+#define PD_T2_WAVES_PER_SIMD 1   // 512 registers: no spills
+#endif
 template <int PROB, class T, int MAXD>
-__global__ __launch_bounds__(64, 2) void tier2_kernel(KernelArgs a) {
+__global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
     constexpr int NC = nc(K);
     using I = ErrInterp<T, K, MAXD>;
