@@ -85,7 +85,15 @@ enum pdeval_opcode {
     PDOP_DIV_X    = 26,  /* top /= x                                             */
     PDOP_DIV_Y    = 27,  /* top /= y                                             */
     PDOP_PUSH_I   = 28,  /* push the imaginary unit (complex pass only)          */
-    PDOP_COUNT_   = 29,
+    /* fused coordinate powers p = v**n: n = operand bits 8-15 (2..16), v = x if bit 16 is
+       0 else y; the jet of p is univariate with C(n,k) v^(n-k) coefficients          */
+    PDOP_PUSH_P   = 29,  /* push p                                               */
+    PDOP_ADD_P    = 30,  /* top += p                                             */
+    PDOP_SUB_P    = 31,  /* top -= p                                             */
+    PDOP_MUL_P    = 32,  /* top *= p                                             */
+    PDOP_DIV_P    = 33,  /* top /= p                                             */
+    PDOP_RDIV_P   = 34,  /* top = p / top                                        */
+    PDOP_COUNT_   = 35,
     PDOP_UNSUPPORTED = 254  /* placeholder for a construct the flattener cannot lower;
                                the candidate is classified PDEVAL_CLS_UNSUPPORTED       */
 };

@@ -159,6 +159,52 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
                 }
                 break;
             }
+            case PDOP_PUSH_P: case PDOP_ADD_P: case PDOP_SUB_P: case PDOP_MUL_P: case PDOP_DIV_P:
+            case PDOP_RDIV_P: {
+                /* p = v**n (v = x or y): its jet by repeated jet products of the coordinate
+                 * (the device uses the closed form C(n,k) v^(n-k)); E_p = n |p| */
+                const int n = (int)((word >> 8) & 0xffu), ax = (int)((word >> 16) & 1u);
+                S v[NCMAX], pj[NCMAX];
+                double ep[NCMAX], P_[NCMAX];
+                FN(jconst)(v, ax ? py : px);
+                v[ax ? IDX(0, 1) : IDX(1, 0)] = 1;
+                memcpy(pj, v, sizeof pj);
+                for (int k = 1; k < n; ++k) FN(jmul)(pj, v, pj, K);
+                if (trk) { FN(wabs)(pj, P_, K); for (int i = 0; i < NC(K); ++i) ep[i] = n * P_[i]; }
+                if (op == PDOP_PUSH_P) {
+                    memcpy(st[d], pj, sizeof(S) * NCMAX);
+                    if (trk) memcpy(es[d], ep, sizeof(double) * NCMAX);
+                    ++d;
+                } else if (op == PDOP_ADD_P || op == PDOP_SUB_P) {
+                    for (int i = 0; i < NC(K); ++i) t[i] = op == PDOP_ADD_P ? t[i] + pj[i] : t[i] - pj[i];
+                    if (trk) for (int i = 0; i < NC(K); ++i) et[i] += ep[i] + cabs(t[i]);
+                } else if (op == PDOP_MUL_P) {
+                    if (trk) {
+                        FN(wabs)(t, A, K);
+                        w_mul(A, ep, T1, K); w_mul(et, P_, T2, K); w_mul(A, P_, R, K);
+                        for (int i = 0; i < NC(K); ++i) et[i] = T1[i] + T2[i] + R[i];
+                    }
+                    FN(jmul)(t, pj, t, K);
+                } else {
+                    /* DIV_P: t = t / p (num t, den p);  RDIV_P: t = p / t (num p, den t) */
+                    const int dv = op == PDOP_DIV_P;
+                    double en[NCMAX], ed[NCMAX];
+                    if (trk) {
+                        memcpy(en, dv ? et : ep, sizeof en);
+                        memcpy(ed, dv ? ep : et, sizeof ed);
+                        if (dv) memcpy(B, P_, sizeof B); else FN(wabs)(t, B, K);
+                    }
+                    if (dv) FN(jdiv)(t, pj, t, K); else FN(jdiv)(pj, t, t, K);
+                    if (trk) {
+                        FN(wabs)(t, R, K);
+                        w_mul(R, ed, A, K);
+                        for (int i = 0; i < NC(K); ++i) A[i] += en[i];
+                        w_absdiv(A, B, et, K);
+                        for (int i = 0; i < NC(K); ++i) et[i] += R[i];
+                    }
+                }
+                break;
+            }
             case PDOP_NEG: for (int i = 0; i < NC(K); ++i) t[i] = -t[i]; break;
             case PDOP_ADD_X: t[0] += px; t[IDX(1, 0)] += 1; if (trk) et[0] += cabs(t[0]); break;
             case PDOP_ADD_Y: t[0] += py; t[IDX(0, 1)] += 1; if (trk) et[0] += cabs(t[0]); break;

@@ -240,7 +240,8 @@ static int op_has_imm(uint32_t op) {
 }
 static int op_stack_delta(uint32_t op, int* need) {
     switch (op) {
-        case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I: case PDOP_UNSUPPORTED:
+        case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I: case PDOP_PUSH_P:
+        case PDOP_UNSUPPORTED:
             *need = 0; return 1;
         case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: case PDOP_MUL: case PDOP_DIV: case PDOP_RDIV:
             *need = 2; return -1;
@@ -261,7 +262,7 @@ extern "C" int pdeval_program_depth(const int32_t* ops, int64_t n_words) {
         const int dd = op_stack_delta(op, &need);
         if (need < 0) return -3;
         if (d < need) return -4;
-        if (op == PDOP_POWN) {
+        if (op == PDOP_POWN || (op >= PDOP_PUSH_P && op <= PDOP_RDIV_P)) {
             const int n = (ops[pc] >> 8) & 0xff;
             if (n < 2 || n > 16) return -5;
         }
@@ -303,6 +304,12 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
                 break;
             }
             case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: f += compf; break;
+            // coordinate powers: K+1 coefficients, then a sparse (univariate) product/quotient
+            case PDOP_PUSH_P: f += 3 * (K + 1); break;
+            case PDOP_ADD_P: case PDOP_SUB_P: f += 4 * (K + 1); break;
+            case PDOP_MUL_P: f += 3 * (K + 1) + (ff ? 50.0 : 14.0); break;
+            case PDOP_DIV_P: f += 3 * (K + 1) + (ff ? 60.0 : 18.0); break;
+            case PDOP_RDIV_P: f += 3 * (K + 1) + divf; break;
             default: break;
         }
         pc += 1 + (op_has_imm(op) ? 2 : 0);

@@ -202,6 +202,97 @@ template <class T, int K> struct JetOps {
             }
         }
     }
+    // ---- coordinate powers p = v^n along an axis (PDOP_*_P): p_k = C(n,k) v^(n-k), k <= K.
+    // Every index below is a compile-time constant after unrolling (axis is a template
+    // parameter, n enters only through values), so the jets stay in registers.
+    template <int N> static PD_HD void pco_small(double v, double* pk) {   // N < K
+        double vp[N + 1];
+        vp[0] = 1.0;
+#pragma unroll
+        for (int k = 1; k <= N; ++k) vp[k] = vp[k - 1] * v;
+        double b = 1.0;
+#pragma unroll
+        for (int k = 0; k <= K; ++k) {
+            pk[k] = k <= N ? b * vp[k <= N ? N - k : 0] : 0.0;
+            b = b * (double)(N - k) / (double)(k + 1);
+        }
+    }
+    static PD_HD void pcoefs(double v, int n, double* pk) {
+        if constexpr (K > 2) {
+            if (n == 2) { pco_small<2>(v, pk); return; }
+        }
+        if constexpr (K > 3) {
+            if (n == 3) { pco_small<3>(v, pk); return; }
+        }
+        double base = 1.0;                  // v^(n-K), n >= K here
+        for (int e = 0; e < n - K; ++e) base *= v;
+        double pw[K + 1];
+        pw[K] = base;
+#pragma unroll
+        for (int k = K - 1; k >= 0; --k) pw[k] = pw[k + 1] * v;
+        double b = 1.0;
+#pragma unroll
+        for (int k = 0; k <= K; ++k) {
+            pk[k] = b * pw[k];
+            b = b * (double)(n - k) / (double)(k + 1);
+        }
+    }
+    template <int AX> static PD_HD constexpr int pidx(int k, int other) { return AX == 0 ? ji(k, other) : ji(other, k); }
+    template <int AX> static PD_HD void set_p(J& t, const double* pk) {
+        set_const(t, from_real<T>(pk[0]));
+#pragma unroll
+        for (int k = 1; k <= K; ++k) t.c[pidx<AX>(k, 0)] = from_real<T>(pk[k]);
+    }
+    template <int AX> static PD_HD void add_p(J& t, const double* pk, double sg) {
+#pragma unroll
+        for (int k = 0; k <= K; ++k) t.c[pidx<AX>(k, 0)] = t.c[pidx<AX>(k, 0)] + from_real<T>(sg * pk[k]);
+    }
+    // t *= p in place (decreasing degree: c_ij reads t at lower orders along the axis)
+    template <int AX> static PD_HD void mul_p(J& t, const double* pk) {
+#pragma unroll
+        for (int d = K; d >= 0; --d) {
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                const int i = d - j;
+                const int ia = AX == 0 ? i : j, io = AX == 0 ? j : i;
+                T s = t.c[ji(i, j)] * pk[0];
+#pragma unroll
+                for (int k = 1; k <= K; ++k)
+                    if (k <= ia) s = fmac(t.c[pidx<AX>(ia - k, io)], from_real<T>(pk[k]), s);
+                t.c[ji(i, j)] = s;
+            }
+        }
+    }
+    // t /= p in place (increasing degree)
+    template <int AX> static PD_HD void div_p(J& t, const double* pk) {
+        const T b0 = from_real<T>(pk[0]);
+        const T inv = from_real<T>(1.0 / pk[0]);
+#pragma unroll
+        for (int d = 0; d <= K; ++d) {
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                const int i = d - j;
+                const int ia = AX == 0 ? i : j, io = AX == 0 ? j : i;
+                T s = t.c[ji(i, j)];
+#pragma unroll
+                for (int k = 1; k <= K; ++k)
+                    if (k <= ia) s = fmac(t.c[pidx<AX>(ia - k, io)], from_real<T>(-pk[k]), s);
+                t.c[ji(i, j)] = qdiv(s, b0, inv);
+            }
+        }
+    }
+    // the opcode's action on the top of stack for a fixed axis
+    template <int AX> static PD_HD void p_op(uint32_t op, J& t, const double* pk) {
+        if (op == PDOP_ADD_P) add_p<AX>(t, pk, 1.0);
+        else if (op == PDOP_SUB_P) add_p<AX>(t, pk, -1.0);
+        else if (op == PDOP_MUL_P) mul_p<AX>(t, pk);
+        else if (op == PDOP_DIV_P) div_p<AX>(t, pk);
+        else {  // RDIV_P: t = p / t
+            J p;
+            set_p<AX>(p, pk);
+            div(p, t);
+        }
+    }
     static PD_HD void rdivc(J& t, T c) {  // t = c / t
         J a;
         set_const(a, c);
@@ -543,6 +634,30 @@ template <class T, int K, int MAXD> struct Interp {
             }
             const uint32_t wn = (npc < end) ? rd_word(ops + npc) : 0u;
             switch (op) {
+                case PDOP_PUSH_P: {
+                    if (d > 0 && d < MAXD) lds_store(stk, d - 1, lane, acc);
+                    double pk[K + 1];
+                    if ((w >> 16) & 1) {
+                        O::pcoefs(y, (int)((w >> 8) & 0xffu), pk);
+                        O::template set_p<1>(acc, pk);
+                    } else {
+                        O::pcoefs(x, (int)((w >> 8) & 0xffu), pk);
+                        O::template set_p<0>(acc, pk);
+                    }
+                    ++d;
+                    break;
+                }
+                case PDOP_ADD_P: case PDOP_SUB_P: case PDOP_MUL_P: case PDOP_DIV_P: case PDOP_RDIV_P: {
+                    double pk[K + 1];
+                    if ((w >> 16) & 1) {
+                        O::pcoefs(y, (int)((w >> 8) & 0xffu), pk);
+                        O::template p_op<1>(op, acc, pk);
+                    } else {
+                        O::pcoefs(x, (int)((w >> 8) & 0xffu), pk);
+                        O::template p_op<0>(op, acc, pk);
+                    }
+                    break;
+                }
                 case PDOP_PUSH_X:
                 case PDOP_PUSH_Y:
                 case PDOP_PUSH_C:

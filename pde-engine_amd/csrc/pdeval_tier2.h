@@ -209,6 +209,65 @@ template <class T, int K, int MAXD> struct ErrInterp {
                     for (int i = 0; i < NC; ++i) ea[i] += R[i];
                     break;
                 }
+                case PDOP_PUSH_P: case PDOP_ADD_P: case PDOP_SUB_P: case PDOP_MUL_P: case PDOP_DIV_P:
+                case PDOP_RDIV_P: {
+                    const int ax = (w >> 16) & 1;
+                    const int n = (int)((w >> 8) & 0xffu);
+                    double pk[K + 1], P[NC], ep[NC];
+                    O::pcoefs(ax ? y : x, n, pk);
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) P[i] = 0.0;
+#pragma unroll
+                    for (int k = 0; k <= K; ++k) P[ax ? ji(0, k) : ji(k, 0)] = fabs(pk[k]);
+#pragma unroll
+                    for (int i = 0; i < NC; ++i) ep[i] = n * P[i];      // E of v**n
+                    if (op == PDOP_PUSH_P) {
+                        if (d > 0 && d < MAXD) st(vs, es, d - 1, lane, acc, ea);
+                        if (ax) O::template set_p<1>(acc, pk);
+                        else O::template set_p<0>(acc, pk);
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) ea[i] = ep[i];
+                        ++d;
+                    } else if (op == PDOP_ADD_P || op == PDOP_SUB_P) {
+                        if (ax) O::template p_op<1>(op, acc, pk);
+                        else O::template p_op<0>(op, acc, pk);
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) ea[i] += ep[i];
+                        E::add_abs(acc.c, ea);
+                    } else if (op == PDOP_MUL_P) {
+                        E::absv(acc.c, A);
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) R[i] = ep[i] + P[i];
+                        E::mul(A, R, R);
+                        E::mul(ea, P, ea);
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) ea[i] += R[i];
+                        if (ax) O::template p_op<1>(op, acc, pk);
+                        else O::template p_op<0>(op, acc, pk);
+                    } else {
+                        // DIV_P: t = t / p (num t, den p);  RDIV_P: t = p / t (num p, den t)
+                        const bool dv = op == PDOP_DIV_P;
+                        double en[NC];
+                        if (dv) {
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) { en[i] = ea[i]; A[i] = ep[i]; B[i] = P[i]; }
+                        } else {
+                            E::absv(acc.c, B);
+#pragma unroll
+                            for (int i = 0; i < NC; ++i) { en[i] = ep[i]; A[i] = ea[i]; }
+                        }
+                        if (ax) O::template p_op<1>(op, acc, pk);
+                        else O::template p_op<0>(op, acc, pk);
+                        E::absv(acc.c, R);
+                        E::mul(R, A, A);
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) A[i] += en[i];
+                        E::absdiv(A, B, ea);
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) ea[i] += R[i];
+                    }
+                    break;
+                }
                 case PDOP_NEG:
                     O::scale(acc, from_real<T>(-1.0));
                     break;

@@ -27,7 +27,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import sympy as sp
 
-from .opcodes import (PDOP, HAS_IMM, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD, FLAG_RATIONAL,
+from .opcodes import (PDOP, HAS_IMM, P_OPS, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD, FLAG_RATIONAL,
                       FLAG_NONSMOOTH2D)
 
 
@@ -39,8 +39,13 @@ class Unsupported(Exception):
 # nodes: ('x',) ('y',) ('i',) ('c', float)
 #        (op, child) for op in neg sqrt exp log abs;  ('pown', child, n);  ('pow', child, alpha)
 #        (op, a, b) for op in add sub mul div
+def _is_pvar(n) -> bool:
+    """A coordinate power x**n / y**n (2 <= n <= 16): fused into PUSH_P / ADD_P / ... ."""
+    return n[0] == 'pown' and n[1][0] in ('x', 'y') and 2 <= n[2] <= 16
+
+
 def _is_leaf(n) -> bool:
-    return n[0] in ('x', 'y', 'c')
+    return n[0] in ('x', 'y', 'c') or _is_pvar(n)
 
 
 def _const(v, rational: bool = True) -> tuple:
@@ -210,7 +215,7 @@ def _need(n) -> int:
     a, b = n[1], n[2]
     if _is_leaf(b) and k in ('add', 'sub', 'mul', 'div'):
         return _need(a)
-    if _is_leaf(a) and k in ('add', 'mul', 'sub') or (k == 'div' and a[0] == 'c'):
+    if _is_leaf(a) and k in ('add', 'mul', 'sub') or (k == 'div' and (a[0] == 'c' or _is_pvar(a))):
         return _need(b)
     na, nb = _need(a), _need(b)
     if na == nb:
@@ -237,8 +242,14 @@ class _Emit:
         elif name in ('ADD', 'SUB', 'RSUB', 'MUL', 'DIV', 'RDIV'):
             self.d -= 1
 
+    @staticmethod
+    def _parg(n) -> int:
+        return n[2] | ((0 if n[1][0] == 'x' else 1) << 8)
+
     def leaf(self, n):
-        if n[0] == 'x':
+        if _is_pvar(n):
+            self.op('PUSH_P', arg=self._parg(n))
+        elif n[0] == 'x':
             self.op('PUSH_X')
         elif n[0] == 'y':
             self.op('PUSH_Y')
@@ -250,6 +261,10 @@ class _Emit:
     def fused(self, k: str, leaf) -> bool:
         """top = top (k) leaf as one opcode, if one exists."""
         t = leaf[0]
+        if _is_pvar(leaf):
+            self.op({'add': 'ADD_P', 'sub': 'SUB_P', 'mul': 'MUL_P', 'div': 'DIV_P'}[k],
+                    arg=self._parg(leaf))
+            return True
         if t == 'c':
             c = leaf[1]
             if k == 'add':
@@ -272,7 +287,7 @@ class _Emit:
 
     def emit(self, n):
         k = n[0]
-        if k in ('x', 'y', 'c', 'i'):
+        if k in ('x', 'y', 'c', 'i') or _is_pvar(n):
             self.leaf(n)
             return
         if k in ('neg', 'sqrt', 'exp', 'log', 'abs'):
@@ -305,6 +320,10 @@ class _Emit:
             self.emit(b)
             self.op('RDIVC', a[1])
             return
+        if k == 'div' and _is_pvar(a):          # v**n / b
+            self.emit(b)
+            self.op('RDIV_P', arg=self._parg(a))
+            return
         na, nb = _need(a), _need(b)
         if na >= nb:
             self.emit(a)
@@ -327,11 +346,6 @@ def lower(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
     lw = _Lower(x_sym, y_sym, consts or {})
     return lw.node(expr), lw.uses_i, not lw.irrational_const
 
-
-_RATIONAL_OPS = {PDOP[k] for k in ('PUSH_X', 'PUSH_Y', 'PUSH_C', 'ADD', 'SUB', 'RSUB', 'MUL', 'DIV',
-                                   'RDIV', 'ADDC', 'MULC', 'RDIVC', 'NEG', 'ADD_X', 'ADD_Y',
-                                   'MUL_X', 'MUL_Y', 'SUB_X', 'SUB_Y', 'DIV_X', 'DIV_Y', 'POWN',
-                                   'ABS')}
 
 
 def _op_positions(body: Sequence[int]):
@@ -443,12 +457,13 @@ def compile_ir(ir, uses_i: bool = False, rational_consts: bool = True) -> List[i
         raise AssertionError('stack imbalance in flattener')
     if em.dmax > MAX_STACK:
         raise Unsupported(f'stack depth {em.dmax} > {MAX_STACK}')
-    coord_ops = {PDOP[k] for k in ('PUSH_X', 'PUSH_Y', 'ADD_X', 'ADD_Y', 'SUB_X', 'SUB_Y',
-                                   'MUL_X', 'MUL_Y', 'DIV_X', 'DIV_Y')}
-    has_coord = any(em.w[i] & 0xff in coord_ops for i in _op_positions(em.w))
-    ops = [em.w[i] & 0xff for i in _op_positions(em.w)]
-    xs = any(o in (PDOP['PUSH_X'], PDOP['ADD_X'], PDOP['SUB_X'], PDOP['MUL_X'], PDOP['DIV_X']) for o in ops)
-    ys = any(o in (PDOP['PUSH_Y'], PDOP['ADD_Y'], PDOP['SUB_Y'], PDOP['MUL_Y'], PDOP['DIV_Y']) for o in ops)
+    words = [em.w[i] for i in _op_positions(em.w)]
+    ops = [w & 0xff for w in words]
+    xops = {PDOP[k] for k in ('PUSH_X', 'ADD_X', 'SUB_X', 'MUL_X', 'DIV_X')}
+    yops = {PDOP[k] for k in ('PUSH_Y', 'ADD_Y', 'SUB_Y', 'MUL_Y', 'DIV_Y')}
+    xs = any(o in xops or (o in P_OPS and not (w >> 16) & 1) for o, w in zip(ops, words))
+    ys = any(o in yops or (o in P_OPS and (w >> 16) & 1) for o, w in zip(ops, words))
+    has_coord = xs or ys
     nonsmooth2d = xs and ys and PDOP['ABS'] in ops
     rational = not uses_i and det_rational(ir)
     hdr = (PDOP['HEADER'] | (em.dmax << 8) | (FLAG_COMPLEX if uses_i else 0)
@@ -482,7 +497,10 @@ def disasm(words: Sequence[int]) -> str:
             out.append(f'{name} {v!r}')
             i += 3
         else:
-            out.append(f'{name}' + (f' {w >> 8}' if op == PDOP['POWN'] else ''))
+            if op in P_OPS:
+                out.append(f"{name} {'xy'[(w >> 16) & 1]}^{(w >> 8) & 0xff}")
+            else:
+                out.append(f'{name}' + (f' {w >> 8}' if op == PDOP['POWN'] else ''))
             i += 1
     return '\n'.join(out)
 

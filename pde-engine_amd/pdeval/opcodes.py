@@ -10,10 +10,13 @@ PDOP = dict(
     ADDC=10, MULC=11, RDIVC=12, NEG=13,
     ADD_X=14, ADD_Y=15, MUL_X=16, MUL_Y=17, SUB_X=18, SUB_Y=19,
     POWN=20, POW=21, EXP=22, LOG=23, ABS=24, SQRT=25,
-    DIV_X=26, DIV_Y=27, PUSH_I=28, UNSUPPORTED=254,
+    DIV_X=26, DIV_Y=27, PUSH_I=28,
+    PUSH_P=29, ADD_P=30, SUB_P=31, MUL_P=32, DIV_P=33, RDIV_P=34, UNSUPPORTED=254,
 )
 OP_NAME = {v: k for k, v in PDOP.items()}
 HAS_IMM = {PDOP['PUSH_C'], PDOP['ADDC'], PDOP['MULC'], PDOP['RDIVC'], PDOP['POW']}
+# opcodes whose operand (bits 8-23) is a coordinate power v**n: n in bits 8-15, axis in bit 16
+P_OPS = {PDOP[k] for k in ('PUSH_P', 'ADD_P', 'SUB_P', 'MUL_P', 'DIV_P', 'RDIV_P')}
 
 PROBLEM_FORCE_FREE = 0
 PROBLEM_KERR = 1

@@ -51,9 +51,9 @@ def test_program_depth_checks():
     pd_ = P.force_free()
     w = np.array(pd_.compile(pd_.parse('sqrt(z**2 + (rho - 1)**2) - sqrt(z**2 + (rho + 1)**2)')),
                  dtype=np.int32)
-    assert _lib.program_depth(w) == 3
+    assert _lib.program_depth(w) == 2           # (rho +- 1)**2 + z**2: z**2 is a fused operand
     bad = w.copy()
-    bad[0] = (bad[0] & ~0xff00) | (2 << 8)      # header lies about the depth
+    bad[0] = (bad[0] & ~0xff00) | (3 << 8)      # header lies about the depth
     assert _lib.program_depth(bad) < 0
     assert _lib.program_depth(w[:-1]) < 0        # truncated: stack not reduced to one value
     assert _lib.program_depth(np.array([0x100, 99], dtype=np.int32)) < 0   # unknown opcode
