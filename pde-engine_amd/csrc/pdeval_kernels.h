@@ -78,7 +78,11 @@ template <> struct Real<cplx> { static constexpr bool cplx_pass = true; };
 // become scalar loads (s_load_dword, served by the scalar cache) instead of vector loads +
 // readfirstlane -- one such dependent load per opcode per chunk was a large share of the
 // interpreter's time.
+#ifndef PD_HOST_SIM
 typedef const __attribute__((address_space(4))) uint32_t* cword_ptr;
+#else
+typedef const uint32_t* cword_ptr;   // tests/hostsim: the interpreter on the CPU, one lane
+#endif
 __device__ __forceinline__ uint32_t rd_word(const int32_t* p) {
     return *(cword_ptr)(p);
 }
@@ -87,6 +91,14 @@ __device__ __forceinline__ double rd_imm(const int32_t* p) {
     const uint32_t lo = *(cword_ptr)(p);
     const uint32_t hi = *(cword_ptr)(p + 1);
     return __hiloint2double((int)hi, (int)lo);
+}
+// a wave-uniform double (grid abscissa) through the scalar cache
+__device__ __forceinline__ double rd_sf64(const double* p) {
+#ifndef PD_HOST_SIM
+    return *(const __attribute__((address_space(4))) double*)(p);
+#else
+    return *p;
+#endif
 }
 __device__ __forceinline__ bool op_has_imm(uint32_t op) {
     return op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC ||
@@ -745,7 +757,11 @@ void validate_kernel(KernelArgs a) {
     using J = typename I::J;
     const int lane = threadIdx.x & 63;
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
     T* stk = reinterpret_cast<T*>(pd_lds) + (size_t)wib * (MAXD - 1) * nc(K) * 64;
     const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
     // persistent variants stride over a device work list; the first pass is one wave per
@@ -811,7 +827,7 @@ void validate_kernel(KernelArgs a) {
                 const int row = (ch - 1) / per_row, sl = (ch - 1) - row * per_row;
                 active = true;
                 p = a.n_ref + row * a.ny + sl * 64 + lane;
-                x = *(const __attribute__((address_space(4))) double*)(a.gx + row);   // scalar
+                x = rd_sf64(a.gx + row);   // scalar
                 y = per_row == 1 ? y_lane : a.gy[sl * 64 + lane];
             }
             const int pp = p;

@@ -392,7 +392,11 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
     using I = ErrInterp<T, K, MAXD>;
     using J = typename I::J;
     const int lane = threadIdx.x & 63;
+#ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
     T* vs = reinterpret_cast<T*>(pd_lds);
     double* es = reinterpret_cast<double*>(pd_lds + (size_t)(MAXD - 1) * NC * 64 * sizeof(T));
     int64_t nwork = (int64_t)(*a.list_count);
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             for (int ch = 0; ch < nchunks; ++ch) {
                 const int row = ch / per_row, sl = ch - row * per_row;
                 const int p = a.n_ref + row * a.ny + sl * 64 + lane;
-                const double x = *(const __attribute__((address_space(4))) double*)(a.gx + row);
+                const double x = rd_sf64(a.gx + row);
                 const double y = a.gy[sl * 64 + lane];
                 J u;
                 double e[NC];
