@@ -179,6 +179,13 @@ int pdeval_pass_times(pdeval_ctx* ctx, float* ms, int max_passes, const char** n
  * [4] tier-2 stack 3, [5] tier-2 complex, [6] complex stack 8, [7] tier-2 stack 8.        */
 int pdeval_pass_counts(pdeval_ctx* ctx, int64_t* counts, int max_counts);
 
+/* Diagnostics (force-free): one program at n_pts points (host arrays), tier-1 (tier2 = 0) or
+ * tier-2 arithmetic; out[4p..4p+3] = {|residual|, S, noise bound (tier 2), finite (1/0,
+ * -1 = program error)}; jets (may be NULL): 30 doubles per point, the 15 Taylor
+ * coefficients of u then their error bounds.  Synchronous; allocates.  Not a hot path.  */
+int pdeval_eval_points(pdeval_ctx* ctx, const int32_t* prog, int64_t n_words, const double* xs,
+                       const double* ys, int n_pts, int tier2, double* out, double* jets);
+
 /* Host-side program analysis (no GPU): required stack depth, or < 0 if malformed.      */
 int pdeval_program_depth(const int32_t* ops, int64_t n_words);
 

@@ -595,3 +595,46 @@ extern "C" int pdeval_pass_counts(pdeval_ctx* c, int64_t* counts, int max_counts
     for (int k = 0; k < max_counts && k < PD_N_LISTS; ++k) counts[k] = h[k];
     return PDEVAL_OK;
 }
+
+extern "C" int pdeval_eval_points(pdeval_ctx* c, const int32_t* prog, int64_t n_words, const double* xs,
+                                  const double* ys, int n_pts, int tier2, double* out, double* jets) {
+    if (!c || !prog || !xs || !ys || !out || n_pts <= 0 || n_pts > (1 << 20)) return PDEVAL_ERR_ARG;
+    const int d = pdeval_program_depth(prog, n_words);
+    if (d < 0 || d > PDEVAL_MAX_STACK) {
+        c->err = "pdeval_eval_points: malformed program";
+        return PDEVAL_ERR_PROGRAM;
+    }
+    if (c->problem == PDEVAL_PROBLEM_KERR) {
+        c->err = "pdeval_eval_points: force-free only";
+        return PDEVAL_ERR_ARG;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    int32_t* d_prog = nullptr;
+    double *d_x = nullptr, *d_y = nullptr, *d_out = nullptr, *d_jets = nullptr;
+    const size_t jet_bytes = (size_t)n_pts * 2 * 15 * sizeof(double);
+    auto cleanup = [&]() {
+        for (void* q : {(void*)d_prog, (void*)d_x, (void*)d_y, (void*)d_out, (void*)d_jets})
+            if (q) (void)hipFree(q);
+    };
+    hipError_t e = hipSuccess;
+    if ((e = hipMalloc(&d_prog, n_words * 4)) == hipSuccess && (e = hipMalloc(&d_x, n_pts * 8)) == hipSuccess &&
+        (e = hipMalloc(&d_y, n_pts * 8)) == hipSuccess && (e = hipMalloc(&d_out, n_pts * 32)) == hipSuccess &&
+        (e = hipMemcpy(d_prog, prog, n_words * 4, hipMemcpyHostToDevice)) == hipSuccess &&
+        (e = hipMemcpy(d_x, xs, n_pts * 8, hipMemcpyHostToDevice)) == hipSuccess &&
+        (e = hipMemcpy(d_y, ys, n_pts * 8, hipMemcpyHostToDevice)) == hipSuccess &&
+        (!jets || (e = hipMalloc(&d_jets, jet_bytes)) == hipSuccess)) {
+        constexpr int K = 4, MAXD = PDEVAL_MAX_STACK;
+        hipLaunchKernelGGL((eval_points_kernel<PDEVAL_PROBLEM_FORCE_FREE, MAXD>), dim3((n_pts + 63) / 64), dim3(64),
+                           (tier2_lds<double, K, MAXD>()), c->stream, d_prog, (int)n_words, d_x, d_y,
+                           (const double*)nullptr, n_pts, tier2, d_out, d_jets);
+        if ((e = hipGetLastError()) == hipSuccess && (e = hipStreamSynchronize(c->stream)) == hipSuccess)
+            e = hipMemcpy(out, d_out, n_pts * 32, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && jets) e = hipMemcpy(jets, d_jets, jet_bytes, hipMemcpyDeviceToHost);
+    }
+    cleanup();
+    if (e != hipSuccess) {
+        c->err = std::string("pdeval_eval_points: ") + hipGetErrorString(e);
+        return PDEVAL_ERR_HIP;
+    }
+    return PDEVAL_OK;
+}

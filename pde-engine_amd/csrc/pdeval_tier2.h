@@ -110,6 +110,46 @@ template <class T, int K, int MAXD> struct ErrInterp {
         }
     }
 
+    // binary op t = a (op) t with error bounds (a = lhs with bound el), op in ADD..RDIV
+    static __device__ __forceinline__ void binop_e(uint32_t op, const J& lhs, const double* el, J& acc, double* ea) {
+        double A[NC], B[NC], R[NC];
+        if (op == PDOP_ADD || op == PDOP_SUB || op == PDOP_RSUB) {
+            Interp<T, K, MAXD>::binop(op, lhs, acc);
+#pragma unroll
+            for (int i = 0; i < NC; ++i) ea[i] += el[i];
+            E::add_abs(acc.c, ea);
+        } else if (op == PDOP_MUL) {
+            // |a| (*) (E_t + |t|) + E_a (*) |t|
+            E::absv(lhs.c, A);
+            E::absv(acc.c, B);
+#pragma unroll
+            for (int i = 0; i < NC; ++i) R[i] = ea[i] + B[i];
+            E::mul(A, R, R);
+            E::mul(el, B, A);
+#pragma unroll
+            for (int i = 0; i < NC; ++i) ea[i] = R[i] + A[i];
+            O::mul(lhs, acc);
+        } else {
+            // DIV: t = a / t (num a, den t);  RDIV: t = t / a (num t, den a)
+            const bool dv = op == PDOP_DIV;
+            E::absv(dv ? acc.c : lhs.c, B);            // |den|
+            double en[NC];
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                en[i] = dv ? el[i] : ea[i];            // E_num
+                A[i] = dv ? ea[i] : el[i];             // E_den
+            }
+            Interp<T, K, MAXD>::binop(op, lhs, acc);
+            E::absv(acc.c, R);
+            E::mul(R, A, A);
+#pragma unroll
+            for (int i = 0; i < NC; ++i) A[i] += en[i];
+            E::absdiv(A, B, ea);
+#pragma unroll
+            for (int i = 0; i < NC; ++i) ea[i] += R[i];
+        }
+    }
+
     // value + error bound of program words [pc, end) at (x, y)
     static __device__ int run(const int32_t* ops, int pc, int end, double x, double y, J& acc,
                               double* ea, T* vs, double* es, int lane) {
@@ -148,41 +188,7 @@ template <class T, int K, int MAXD> struct ErrInterp {
                         J lhs;
                         double el[NC];
                         ld(vs, es, d - 2, lane, lhs, el);
-                        if (op == PDOP_ADD || op == PDOP_SUB || op == PDOP_RSUB) {
-                            Interp<T, K, MAXD>::binop(op, lhs, acc);
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) ea[i] += el[i];
-                            E::add_abs(acc.c, ea);
-                        } else if (op == PDOP_MUL) {
-                            // |a| (*) (E_t + |t|) + E_a (*) |t|
-                            E::absv(lhs.c, A);
-                            E::absv(acc.c, B);
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) R[i] = ea[i] + B[i];
-                            E::mul(A, R, R);
-                            E::mul(el, B, A);
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) ea[i] = R[i] + A[i];
-                            O::mul(lhs, acc);
-                        } else {
-                            // DIV: t = a / t (num a, den t);  RDIV: t = t / a (num t, den a)
-                            const bool dv = op == PDOP_DIV;
-                            E::absv(dv ? acc.c : lhs.c, B);            // |den|
-                            double en[NC];
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) {
-                                en[i] = dv ? el[i] : ea[i];            // E_num
-                                A[i] = dv ? ea[i] : el[i];             // E_den
-                            }
-                            Interp<T, K, MAXD>::binop(op, lhs, acc);
-                            E::absv(acc.c, R);
-                            E::mul(R, A, A);
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) A[i] += en[i];
-                            E::absdiv(A, B, ea);
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) ea[i] += R[i];
-                        }
+                        binop_e(op, lhs, el, acc, ea);
                     }
                     --d;
                     break;
@@ -211,60 +217,30 @@ template <class T, int K, int MAXD> struct ErrInterp {
                 }
                 case PDOP_PUSH_P: case PDOP_ADD_P: case PDOP_SUB_P: case PDOP_MUL_P: case PDOP_DIV_P:
                 case PDOP_RDIV_P: {
-                    const int ax = (w >> 16) & 1;
+                    // p = v**n as a (value, bound) operand of the generic binary ops; E_p = n |p|
                     const int n = (int)((w >> 8) & 0xffu);
-                    double pk[K + 1], P[NC], ep[NC];
-                    O::pcoefs(ax ? y : x, n, pk);
+                    double pk[K + 1], ep[NC];
+                    J p;
+                    if ((w >> 16) & 1) {
+                        O::pcoefs(y, n, pk);
+                        O::template set_p<1>(p, pk);
+                    } else {
+                        O::pcoefs(x, n, pk);
+                        O::template set_p<0>(p, pk);
+                    }
 #pragma unroll
-                    for (int i = 0; i < NC; ++i) P[i] = 0.0;
-#pragma unroll
-                    for (int k = 0; k <= K; ++k) P[ax ? ji(0, k) : ji(k, 0)] = fabs(pk[k]);
-#pragma unroll
-                    for (int i = 0; i < NC; ++i) ep[i] = n * P[i];      // E of v**n
+                    for (int i = 0; i < NC; ++i) ep[i] = n * mag(p.c[i]);
                     if (op == PDOP_PUSH_P) {
                         if (d > 0 && d < MAXD) st(vs, es, d - 1, lane, acc, ea);
-                        if (ax) O::template set_p<1>(acc, pk);
-                        else O::template set_p<0>(acc, pk);
+                        acc = p;
 #pragma unroll
                         for (int i = 0; i < NC; ++i) ea[i] = ep[i];
                         ++d;
-                    } else if (op == PDOP_ADD_P || op == PDOP_SUB_P) {
-                        if (ax) O::template p_op<1>(op, acc, pk);
-                        else O::template p_op<0>(op, acc, pk);
-#pragma unroll
-                        for (int i = 0; i < NC; ++i) ea[i] += ep[i];
-                        E::add_abs(acc.c, ea);
-                    } else if (op == PDOP_MUL_P) {
-                        E::absv(acc.c, A);
-#pragma unroll
-                        for (int i = 0; i < NC; ++i) R[i] = ep[i] + P[i];
-                        E::mul(A, R, R);
-                        E::mul(ea, P, ea);
-#pragma unroll
-                        for (int i = 0; i < NC; ++i) ea[i] += R[i];
-                        if (ax) O::template p_op<1>(op, acc, pk);
-                        else O::template p_op<0>(op, acc, pk);
                     } else {
-                        // DIV_P: t = t / p (num t, den p);  RDIV_P: t = p / t (num p, den t)
-                        const bool dv = op == PDOP_DIV_P;
-                        double en[NC];
-                        if (dv) {
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) { en[i] = ea[i]; A[i] = ep[i]; B[i] = P[i]; }
-                        } else {
-                            E::absv(acc.c, B);
-#pragma unroll
-                            for (int i = 0; i < NC; ++i) { en[i] = ep[i]; A[i] = ea[i]; }
-                        }
-                        if (ax) O::template p_op<1>(op, acc, pk);
-                        else O::template p_op<0>(op, acc, pk);
-                        E::absv(acc.c, R);
-                        E::mul(R, A, A);
-#pragma unroll
-                        for (int i = 0; i < NC; ++i) A[i] += en[i];
-                        E::absdiv(A, B, ea);
-#pragma unroll
-                        for (int i = 0; i < NC; ++i) ea[i] += R[i];
+                        // ADD_P: p + t;  SUB_P: t - p;  MUL_P: p * t;  DIV_P: t / p;  RDIV_P: p / t
+                        const uint32_t bop = op == PDOP_ADD_P ? PDOP_ADD : op == PDOP_SUB_P ? PDOP_RSUB
+                                           : op == PDOP_MUL_P ? PDOP_MUL : op == PDOP_DIV_P ? PDOP_RDIV : PDOP_DIV;
+                        binop_e(bop, p, ep, acc, ea);
                     }
                     break;
                 }
@@ -501,4 +477,52 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
     }
 }
 
+}  // namespace pd
+
+namespace pd {
+// Diagnostic / test kernel: one program at a list of points (lane = point), tier-1 or tier-2
+// arithmetic; out[4 p ..] = {|residual|, S, noise (tier 2), finite}.  Used by the GPU parity
+// tests to compare the device's point arithmetic with the oracle's directly.
+template <int PROB, int MAXD>
+__global__ __launch_bounds__(64, 1) void eval_points_kernel(const int32_t* prog, int plen, const double* xs,
+                                                            const double* ys, const double* kc, int npts, int tier2,
+                                                            double* out, double* jets) {
+    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
+    constexpr int NC = nc(K);
+    using EI = ErrInterp<double, K, MAXD>;
+    using I = Interp<double, K, MAXD>;
+    const int lane = threadIdx.x & 63;
+#ifndef PD_HOST_SIM
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
+    double* vs = reinterpret_cast<double*>(pd_lds);
+    double* es = vs + (size_t)(MAXD - 1) * NC * 64;
+    const int p = blockIdx.x * 64 + lane;
+    const int pc = p < npts ? p : npts - 1;
+    const double x = xs[pc], y = ys[pc];
+    typename I::J u;
+    double e[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) e[i] = 0.0;
+    const int rc = tier2 ? EI::run(prog, 1, plen, x, y, u, e, vs, es, lane) : I::run(prog, 1, plen, x, y, u, vs, lane);
+    PointResult r;
+    const double* k4 = kc ? kc + 4 * pc : nullptr;
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);
+    else r = kerr_epilogue<double>(u.c, k4);
+    if (p < npts) {
+        out[4 * p + 0] = rc ? NAN : r.res_abs;
+        out[4 * p + 1] = rc ? NAN : r.scale;
+        out[4 * p + 2] = (rc || !tier2) ? 0.0 : residual_noise<PROB, double>(u.c, e, x, k4, r.scale);
+        out[4 * p + 3] = rc ? -1.0 : (r.finite ? 1.0 : 0.0);
+        if (jets) {
+#pragma unroll
+            for (int i = 0; i < NC; ++i) {
+                jets[(size_t)p * 2 * NC + i] = u.c[i];
+                jets[(size_t)p * 2 * NC + NC + i] = e[i];
+            }
+        }
+    }
+}
 }  // namespace pd

@@ -22,7 +22,7 @@ EXPORTS = (
     'pdeval_create', 'pdeval_destroy', 'pdeval_last_error', 'pdeval_n_ref_points',
     'pdeval_n_points', 'pdeval_default_params', 'pdeval_validate_batch',
     'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
-    'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts',
+    'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts', 'pdeval_eval_points',
 )
 LIST_NAMES = ('defer_stack3', 'complex', 'defer_stack8', 'tier2', 'tier2_stack3', 'tier2_complex',
               'complex_stack8', 'tier2_stack8')
@@ -76,6 +76,7 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_set_timing.argtypes = [vp, C.c_int]
     lib.pdeval_pass_times.argtypes = [vp, vp, C.c_int, vp]
     lib.pdeval_pass_counts.argtypes = [vp, vp, C.c_int]
+    lib.pdeval_eval_points.argtypes = [vp, vp, i64, vp, vp, C.c_int, C.c_int, vp, vp]
     for name in EXPORTS:
         getattr(lib, name)   # every symbol of the header must resolve
     if path is None:
@@ -165,6 +166,18 @@ class Context:
         names = (C.c_char_p * N_PASSES)()
         _check(self.h, self.lib.pdeval_pass_times(self.h, ms, N_PASSES, names))
         return {names[k].decode(): float(ms[k]) for k in range(N_PASSES)}
+
+    def eval_points(self, words, xs, ys, tier2: bool = True, jets: bool = False):
+        """(n, 4) array {|residual|, S, noise, finite} of one program at the given points
+        (and, with jets=True, an (n, 2, 15) array of u's coefficients and error bounds)."""
+        w = np.ascontiguousarray(words, dtype=np.int32)
+        x = np.ascontiguousarray(xs, dtype=np.float64)
+        y = np.ascontiguousarray(ys, dtype=np.float64)
+        out = np.zeros((len(x), 4))
+        jt = np.zeros((len(x), 2, 15)) if jets else None
+        _check(self.h, self.lib.pdeval_eval_points(self.h, _ptr(w), w.size, _ptr(x), _ptr(y), len(x),
+                                                   int(tier2), _ptr(out), _ptr(jt)))
+        return (out, jt) if jets else out
 
     def pass_counts(self):
         """{work list: entries} of the most recent call (synchronizes)."""
