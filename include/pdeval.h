@@ -171,7 +171,7 @@ int pdeval_validate_device(pdeval_ctx* ctx, const int32_t* d_ops, int64_t n_word
  * the launch stream (passes a problem does not run take 0 ms).  pdeval_pass_times waits for
  * the last event of the most recent call and writes min(max_passes, PDEVAL_N_PASSES)
  * durations in ms (and, if names != NULL, a static name per pass).                       */
-#define PDEVAL_N_PASSES 9
+#define PDEVAL_N_PASSES 10
 int pdeval_set_timing(pdeval_ctx* ctx, int enable);
 int pdeval_pass_times(pdeval_ctx* ctx, float* ms, int max_passes, const char** names);
 /* Work-list sizes of the most recent call (synchronizes the device): [0] deferred to the

@@ -50,6 +50,7 @@ struct pdeval_ctx {
     // device work lists (capacity cap each) and their counters d_counts[L_*]
     int64_t* d_list[PD_N_LISTS] = {};
     int32_t* d_counts = nullptr;
+    uint8_t* d_pstate = nullptr;    // pass-0 point-stage state, capacity cap
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -65,7 +66,7 @@ struct pdeval_ctx {
 };
 
 static const char* const kPassNames[PDEVAL_N_PASSES] = {
-    "pass1_stack2", "pass2_stack3", "pass3_stack8", "complex_stack2", "complex_stack8",
+    "pass0_point", "pass1_stack2", "pass2_stack3", "pass3_stack8", "complex_stack2", "complex_stack8",
     "tier2_stack2", "tier2_stack3", "tier2_stack8", "tier2_complex"};
 
 static thread_local std::string g_err;
@@ -204,6 +205,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (int64_t* l : c->d_list)
         if (l) (void)hipFree(l);
+    if (c->d_pstate) (void)hipFree(c->d_pstate);
     for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) hipFree(p);
@@ -329,6 +331,9 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     c->cap = 0;
     const int64_t cap = n < 1024 ? 1024 : n;
     for (int64_t*& l : c->d_list) HIPCHK(c, hipMalloc(&l, cap * sizeof(int64_t)));
+    if (c->d_pstate) (void)hipFree(c->d_pstate);
+    c->d_pstate = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_pstate, cap));
     c->cap = cap;
     return PDEVAL_OK;
 }
@@ -398,17 +403,24 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.cplx_count = cnt + L_CPLX;
     a.esc_list = c->d_list[L_ESC];
     a.esc_count = cnt + L_ESC;
+    a.pstate = c->d_pstate;
+    // pass 0: the point stage of every real candidate of stack <= 2, one candidate per lane
+    // (tier 1 + tier 2 at the reference points); complex-valued ones go to L_CPLX
     mark(0);
+    hipLaunchKernelGGL((point_kernel<PROB>), dim3((unsigned)((n + 255) / 256)), dim3(256),
+                       (size_t)4 * 2 * nc(K) * 64 * sizeof(double), s, a);
+    HIPCHK(c, hipGetLastError());
+    mark(1);
     hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256),
                        (stack_lds<double, K, 2>(4)), s, a);
     HIPCHK(c, hipGetLastError());
     // pass 2: stack 3 (7 % of force-free depth 4; 2 LDS slots keep 10 waves per CU)
-    mark(1);
+    mark(2);
     hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3(pgrid), dim3(64),
                        (stack_lds<double, K, 3>(1)), s, follow(L_DEFER, L_DEFER2, L_ESC));
     HIPCHK(c, hipGetLastError());
     // pass 3: stack 4..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
-    mark(2);
+    mark(3);
     hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
                        dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
                        (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
@@ -416,41 +428,41 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     if constexpr (FF) {
         // complex passes: candidates not real at the reference point, in complex arithmetic
         // (SymPy evaluates the point exactly, in the complex field: validator.py:363-402)
-        mark(3);
+        mark(4);
         hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3(pgrid), dim3(64),
                            (stack_lds<cplx, K, 2>(1)), s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C));
         HIPCHK(c, hipGetLastError());
-        mark(4);
+        mark(5);
         hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),
                            dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
                            (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
         HIPCHK(c, hipGetLastError());
     } else {
-        mark(3);
         mark(4);
+        mark(5);
     }
     // tier 2 (pdeval_tier2.h): re-decide every tier-1 failure with error bounds, by stack depth
     KernelArgs t = follow(L_ESC, L_ESC_DEEP, L_ESC);
-    mark(5);
+    mark(6);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, 2>), dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(64),
                        (tier2_lds<double, K, 2>()), s, t);
     HIPCHK(c, hipGetLastError());
-    mark(6);
+    mark(7);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, 3>), dim3((unsigned)std::min<int64_t>(n, 4096)), dim3(64),
                        (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
     HIPCHK(c, hipGetLastError());
-    mark(7);
+    mark(8);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
                        dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, follow(L_ESC_DEEP2, -1, L_ESC));
     HIPCHK(c, hipGetLastError());
     if constexpr (FF) {
         // (complex programs deeper than 4 keep their tier-1 class: 161 KiB of LDS would not fit)
-        mark(8);
+        mark(9);
         hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4>), dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(64),
                            (tier2_lds<cplx, K, 4>()), s, follow(L_ESC_C, -1, L_ESC_C));
         HIPCHK(c, hipGetLastError());
     } else {
-        mark(8);
+        mark(9);
     }
     mark(PDEVAL_N_PASSES);
     c->ev_recorded = c->timing ? 1 : 0;

@@ -47,6 +47,7 @@ struct KernelArgs {
     int64_t list_capacity;      // capacity of defer_list and cplx_list (appends beyond are dropped)
     int64_t* esc_list;          // tier-2 escalations: cand | ESC_* flags << 48
     int32_t* esc_count;
+    uint8_t* pstate;            // pass-0 point-stage state per candidate (P0_*), or NULL
 };
 
 // Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).
@@ -57,6 +58,9 @@ enum : uint32_t {
     ESC_ANY_GRAD = 8,   // tier 1 saw a finite point with a non-zero gradient
     ESC_NFIN = 16,      // tier 1 saw at least one finite grid point
 };
+// Pass-0 point-stage state per candidate (point_kernel in pdeval_tier2.h)
+enum : uint8_t { P0_NONE = 0, P0_PASS = 1, P0_REJECT = 2, P0_CPLX = 3, P0_GRAD = 16 };
+
 #define PD_ESC_SHIFT 48
 #define PD_ESC_CAND_MASK ((1ll << PD_ESC_SHIFT) - 1)
 
@@ -782,8 +786,16 @@ void validate_kernel(KernelArgs a) {
         const uint32_t hdr = in_bounds ? rd_word(prog) : 0xffu;
         int status = -1;
         if ((hdr & 0xffu) != 0u) status = PDEVAL_CLS_BAD_PROGRAM;
+        // pass 0 decided the point stage of most real candidates (P0_*)
+        uint8_t ps = P0_NONE;
         if constexpr (!Real<T>::cplx_pass) {
-            if (status < 0 && (hdr & PDEVAL_FLAG_COMPLEX)) {
+            if (a.pstate) ps = (uint8_t)__builtin_amdgcn_readfirstlane((int)a.pstate[cand]);
+        }
+        if ((ps & 3) == P0_CPLX) continue;                        // the complex pass takes it
+        if ((ps & 3) == P0_REJECT && !a.prm.full_grid) continue;  // final after pass 0
+        const bool p0 = (ps & 3) != P0_NONE;
+        if constexpr (!Real<T>::cplx_pass) {
+            if (status < 0 && !p0 && (hdr & PDEVAL_FLAG_COMPLEX)) {
                 if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
                     // complex-valued program: straight to the complex pass
                     if (lane == 0 && a.cplx_list) list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
@@ -803,17 +815,17 @@ void validate_kernel(KernelArgs a) {
             status = PDEVAL_CLS_UNSUPPORTED;  // deeper than the last variant takes
         }
         double q_ref = 0.0;        // FF: q*, Kerr: max |lhs| over reference points
-        bool point_reject = false;
-        bool point_final = false;  // non-finite at a reference point: no tier 2
+        bool point_reject = (ps & 3) == P0_REJECT;
+        bool point_final = p0;     // non-finite at a reference point, or decided by pass 0: no tier 2
         bool grid_eval = true;
         double qmax = 0.0;
         int nbad = 0, nnonfin = 0, nfin = 0;
-        bool grad_nz = false;
+        bool grad_nz = (ps & P0_GRAD) != 0;
         // chunk 0: the reference points; chunks 1..: one 64-point slice of a grid row each
         const int per_row = a.ny >> 6;
         const int nchunks = 1 + a.nx * per_row;
         const double y_lane = a.gy[lane];  // row slice 0; other slices reload below
-        for (int ch = 0; ch < nchunks && status < 0; ++ch) {
+        for (int ch = p0 ? 1 : 0; ch < nchunks && status < 0; ++ch) {
             bool active;
             int p;               // point index: reference points first, then the grid row-major
             double x, y;
@@ -935,7 +947,7 @@ void validate_kernel(KernelArgs a) {
                 }
             }
             if (a.out.status) a.out.status[cand] = (uint8_t)cls;
-            if (a.out.q_ref) a.out.q_ref[cand] = q_ref;
+            if (a.out.q_ref && !p0) a.out.q_ref[cand] = q_ref;
             if (a.out.q_grid) a.out.q_grid[cand] = qmax;
             if (a.out.n_bad) a.out.n_bad[cand] = nbad;
             if (a.out.n_nonfinite) a.out.n_nonfinite[cand] = nnonfin;

@@ -151,18 +151,24 @@ template <class T, int K, int MAXD> struct ErrInterp {
     }
 
     // value + error bound of program words [pc, end) at (x, y)
+    // VEC: the program is per lane (pass 0, one candidate per lane): vector loads; otherwise it
+    // is wave-uniform and read through the scalar cache
+    template <bool VEC = false>
     static __device__ int run(const int32_t* ops, int pc, int end, double x, double y, J& acc,
                               double* ea, T* vs, double* es, int lane) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
         for (;;) {
-            const uint32_t w = rd_word(ops + pc);
+            uint32_t w;
+            if constexpr (VEC) w = (uint32_t)ops[pc];
+            else w = rd_word(ops + pc);
             const uint32_t op = w & 0xffu;
             double imm = 0.0;
             int npc = pc + 1;
             if (op_has_imm(op)) {
                 if (pc + 3 > end) return RUN_BAD;
-                imm = rd_imm(ops + pc + 1);
+                if constexpr (VEC) imm = __hiloint2double(ops[pc + 2], ops[pc + 1]);
+                else imm = rd_imm(ops + pc + 1);
                 npc = pc + 3;
             }
             double A[NC], B[NC], R[NC];
@@ -506,7 +512,8 @@ __global__ __launch_bounds__(64, 1) void eval_points_kernel(const int32_t* prog,
     double e[NC];
 #pragma unroll
     for (int i = 0; i < NC; ++i) e[i] = 0.0;
-    const int rc = tier2 ? EI::run(prog, 1, plen, x, y, u, e, vs, es, lane) : I::run(prog, 1, plen, x, y, u, vs, lane);
+    const int rc = tier2 ? EI::template run<false>(prog, 1, plen, x, y, u, e, vs, es, lane)
+                         : I::run(prog, 1, plen, x, y, u, vs, lane);
     PointResult r;
     const double* k4 = kc ? kc + 4 * pc : nullptr;
     if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);
@@ -523,6 +530,113 @@ __global__ __launch_bounds__(64, 1) void eval_points_kernel(const int32_t* prog,
                 jets[(size_t)p * 2 * NC + NC + i] = e[i];
             }
         }
+    }
+}
+}  // namespace pd
+
+namespace pd {
+// Pass 0 (the point stage): one candidate per LANE.  Every real candidate of stack <= 2 is
+// evaluated at the reference point(s) with the error-bounded interpreter (tier 1 and tier 2
+// in one go, as tier2_kernel's point stage), so the point verdict -- the reference's first
+// stage, validator.py:349-402 / kerr :163-192 -- is final here:
+//   pstate[cand] = P0_PASS | P0_REJECT | P0_CPLX (appended to the complex list) | 0 (not taken:
+//   deeper stack, malformed, ...; pass 1 then runs its own point stage), + P0_GRAD if a
+// reference point has a non-zero gradient.  The lanes of a wave interpret different programs
+// (divergent dispatch), which is still ~64x the lane use of one wave per candidate.
+
+template <int PROB>
+__global__ __launch_bounds__(256, 1) void point_kernel(KernelArgs a) {
+    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
+    constexpr int NC = nc(K);
+    constexpr int MAXD = 2;
+    using EI = ErrInterp<double, K, MAXD>;
+    using J = typename EI::J;
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+#ifndef PD_HOST_SIM
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
+    double* vs = reinterpret_cast<double*>(pd_lds) + (size_t)wib * 2 * (MAXD - 1) * NC * 64;
+    double* es = vs + (size_t)(MAXD - 1) * NC * 64;
+    const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cand >= a.n) return;
+    const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
+    uint8_t ps = P0_NONE;
+    const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24);
+    if (in_bounds) {
+        const int32_t* prog = a.ops + beg;
+        const uint32_t hdr = (uint32_t)prog[0];
+        const int depth = (int)((hdr >> 8) & 0xffu);
+        if ((hdr & 0xffu) == 0u && depth <= MAXD) {
+            if (hdr & PDEVAL_FLAG_COMPLEX) {
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+                    if (a.cplx_list) {
+                        list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
+                        ps = P0_CPLX;
+                    }
+                } else {
+                    ps = P0_REJECT;          // Kerr: non-real at a test point (kerr validator.py:179-180)
+                }
+            } else {
+                double qr = 0.0;
+                bool nonfinite = false, reject = false, grad = false, prog_err = false;
+                for (int p = 0; p < a.n_ref; ++p) {
+                    const double x = p == 0 ? a.ref_x[0] : (p == 1 ? a.ref_x[1] : (p == 2 ? a.ref_x[2] : a.ref_x[3]));
+                    const double y = p == 0 ? a.ref_y[0] : (p == 1 ? a.ref_y[1] : (p == 2 ? a.ref_y[2] : a.ref_y[3]));
+                    J u;
+                    double e[NC];
+                    const int rc = EI::template run<true>(prog, 1, (int)(end - beg), x, y, u, e, vs, es, lane);
+                    if (rc != RUN_OK) { prog_err = true; break; }
+                    const double* kc = a.kc ? a.kc + 4 * p : nullptr;
+                    PointResult r;
+                    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);
+                    else r = kerr_epilogue<double>(u.c, kc);
+                    if (p == 0 && a.out.fingerprint) a.out.fingerprint[cand * PDEVAL_FP_N] = u.c[0];
+                    if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = r.res_re;
+                    if (!r.finite) { nonfinite = true; continue; }
+                    if (!r.grad_zero) grad = true;
+                    double v;
+                    bool fails;
+                    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+                        v = scaled(r.res_abs, r.scale);
+                        fails = !(v <= a.prm.tau_point);
+                    } else {
+                        v = r.res_abs;
+                        fails = !(v < a.prm.kerr_abs_tol);
+                    }
+                    qr = fmax(qr, v);
+                    if (fails && r.res_abs > a.prm.noise_kappa * residual_noise<PROB, double>(u.c, e, x, kc, r.scale))
+                        reject = true;
+                }
+                if (!prog_err) {
+                    if (a.out.q_ref) a.out.q_ref[cand] = qr;
+                    if (nonfinite) {
+                        if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+                            // not real at p*: the complex pass decides (validator.py:363-402)
+                            if (a.cplx_list) {
+                                list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
+                                ps = P0_CPLX;
+                            }
+                        } else {
+                            ps = P0_REJECT;  // Kerr: non-real / NaN at a test point
+                        }
+                    } else {
+                        ps = reject ? P0_REJECT : P0_PASS;
+                    }
+                    if (grad) ps |= P0_GRAD;
+                }
+            }
+        }
+    }
+    a.pstate[cand] = ps;
+    if ((ps & 3) == P0_REJECT && !a.prm.full_grid) {
+        // the reference's control flow: a point-stage reject is final
+        if (a.out.status) a.out.status[cand] = PDEVAL_CLS_REJECT_POINT;
+        if (a.out.q_grid) a.out.q_grid[cand] = 0.0;
+        if (a.out.n_bad) a.out.n_bad[cand] = 0;
+        if (a.out.n_nonfinite) a.out.n_nonfinite[cand] = 0;
     }
 }
 }  // namespace pd

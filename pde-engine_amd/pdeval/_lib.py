@@ -26,7 +26,7 @@ EXPORTS = (
 )
 LIST_NAMES = ('defer_stack3', 'complex', 'defer_stack8', 'tier2', 'tier2_stack3', 'tier2_complex',
               'complex_stack8', 'tier2_stack8')
-N_PASSES = 9
+N_PASSES = 10
 
 
 class Params(C.Structure):
