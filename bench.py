@@ -260,6 +260,24 @@ def main():
             res['solutions'] = {k: v for k, v in rec.found.items()}
             res['solution_stream_hits'] = rec.stream_hits
             res['time_to_7_breakdown_s'] = {k: round(v, 4) for k, v in rec.seconds.items()}
+            # the same, starting from the candidate strings instead of compiled programs: the
+            # native compiler (csrc/pdcompile.cpp) plus SymPy for the strings it declines
+            from pdeval import native
+            strs = [str(s) for s in exprs_all]
+            t0 = time.perf_counter()
+            _, _, st_n = native.compile_native(pid, strs)
+            t_nat = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            cst = {}
+            s_ops, s_off, _ = native.compile_strings(P.force_free(), strs, stats=cst)
+            t_comp = time.perf_counter() - t0
+            rec2 = find_known_solutions(ctx, P.force_free(), s_ops, s_off, exprs_all)
+            res['time_to_7_from_strings_s'] = time.perf_counter() - t0
+            res['solutions_found_from_strings'] = rec2.n_found
+            res['compile_from_strings'] = {
+                'strings': len(strs), 'native': cst['native'], 'sympy_fallback': cst['host'],
+                'native_only_s': round(t_nat, 4), 'native_strings_per_s': round(len(strs) / t_nat),
+                'hybrid_compile_s': round(t_comp, 4)}
 
     if rank == 0:
         if not a.no_cpu and world == 1:

@@ -194,6 +194,27 @@ double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words)
 
 const char* pdeval_version(void);
 
+/* ---- native candidate compiler (host only, no GPU; pdcompile.cpp) ----
+ * Replaces, per candidate, the reference's parse  sp.sympify(expr_str, locals=symbols ∪
+ * constants ∪ UNARY_OPS)  (general_method_paper_reproduction.py:84-93, :1257, :1767) plus
+ * this build's lowering of the tree (pdeval/flatten.py).  Strings are concatenated in
+ * text[str_offsets[i] .. str_offsets[i+1]).  Per string, status[i] is
+ *   PDEVAL_COMPILE_OK        program written to ops[offsets[i] .. offsets[i+1])
+ *   PDEVAL_COMPILE_DECLINED  outside the SymPy evaluation rules restated natively (floats,
+ *                            I/E/pi, log, irrational numeric powers, sign-dependent Abs ...):
+ *                            compile this one through SymPy (empty slot)
+ *   PDEVAL_COMPILE_PARSE     not an expression (empty slot; SymPy fails on it too)
+ * Returns PDEVAL_ERR_ARG (and *n_words_out = -1) if ops_cap words are not enough.       */
+#define PDEVAL_COMPILE_OK        0
+#define PDEVAL_COMPILE_DECLINED  1
+#define PDEVAL_COMPILE_PARSE     2
+int pdeval_compile_batch(int problem_id, const char* text, const int64_t* str_offsets, int64_t n,
+                         int32_t* ops, int64_t ops_cap, int64_t* offsets, int32_t* status,
+                         int64_t* n_words_out);
+/* Canonical form of the evaluated expression tree of one string (parity tests against
+ * SymPy's tree): returns a PDEVAL_COMPILE_* status, or -1 on a bad argument / small buffer. */
+int pdeval_canonical(int problem_id, const char* s, int64_t len, char* out, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,1192 @@
+// pdcompile.cpp -- native candidate compiler: candidate string -> postfix jet program.
+//
+// The host half of the hot path.  The reference turns each
+// normalized candidate string into a SymPy tree with
+//     sp.sympify(expr_str, locals=symbols ∪ constants ∪ UNARY_OPS)
+// (general_method_paper_reproduction.py:84-93, :1257, :1703-1714, :1767) and hands the tree
+// to validate(); pde-engine_amd/pdeval/flatten.py lowers that tree to a program.  SymPy costs
+// ~1 ms per candidate, which caps the feed rate of a GPU that validates millions per second.
+//
+// This file does the same in C++, without SymPy:
+//   1. a Python-precedence parser of the string (the grammar SymPy's str() and the
+//      generator's op splices produce: integers, rho/z or r/x/M/a, + - * / **, unary -,
+//      sqrt/exp/Abs and the op names of expression_operations.py:11-77);
+//   2. the part of SymPy's automatic evaluation these strings exercise, restated on a small
+//      hash-consed expression DAG: Add.flatten (like terms), Mul.flatten (like bases,
+//      2-arg Rational*Add distribution), Pow.__new__/_eval_power (integer powers, nested
+//      powers under the real/positive assumptions of problems/__init__.py:70-71, :263-266,
+//      Mul bases split by Pow._eval_expand_power_base), exp powers and Abs.eval;
+//   3. the lowering and Sethi-Ullman emission of flatten.py (same IR, same opcodes, same
+//      header flags including det_rational).
+// Anything outside what is restated exactly (floats, I, E, pi, log, zoo, irrational numeric
+// powers, symbolic exponents, Abs of an argument whose sign SymPy would rewrite ...) is
+// DECLINED: the caller compiles that string through SymPy instead (pdeval/native.py), so a
+// declined string costs what it costs today and every accepted one matches SymPy's tree.
+// Parity: tests/test_native_compile.py compares the canonical form of the DAG with SymPy's
+// tree on the committed candidate streams, and the programs' verdicts with the SymPy path.
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <deque>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pdeval.h"
+
+namespace {
+
+struct Decline {};      // construct outside the exactly-restated subset: compile on the host
+struct ParseError {};   // not an expression SymPy would parse either
+
+// ------------------------------------------------------------------ exact rationals
+struct Rat {
+    int64_t p = 0, q = 1;
+};
+const int64_t kRatMax = (int64_t)1 << 52;   // keep p, q exactly representable as doubles
+Rat mkrat(__int128 p, __int128 q) {
+    if (q == 0) throw Decline{};
+    if (q < 0) { p = -p; q = -q; }
+    __int128 a = p < 0 ? -p : p, b = q;
+    while (b) { __int128 t = a % b; a = b; b = t; }
+    if (a > 1) { p /= a; q /= a; }
+    if (p > kRatMax || p < -kRatMax || q > kRatMax) throw Decline{};
+    return Rat{(int64_t)p, (int64_t)q};
+}
+Rat radd(Rat a, Rat b) { return mkrat((__int128)a.p * b.q + (__int128)b.p * a.q, (__int128)a.q * b.q); }
+Rat rmul(Rat a, Rat b) { return mkrat((__int128)a.p * b.p, (__int128)a.q * b.q); }
+Rat rneg(Rat a) { return Rat{-a.p, a.q}; }
+bool req(Rat a, Rat b) { return a.p == b.p && a.q == b.q; }
+bool rint(Rat a) { return a.q == 1; }
+int rcmp(Rat a, Rat b) {  // sign of a - b
+    __int128 d = (__int128)a.p * b.q - (__int128)b.p * a.q;
+    return d < 0 ? -1 : (d > 0 ? 1 : 0);
+}
+Rat rabs(Rat a) { return Rat{a.p < 0 ? -a.p : a.p, a.q}; }
+Rat rpow_int(Rat b, int64_t n) {
+    if (n < 0) {
+        if (b.p == 0) throw Decline{};   // zoo
+        b = mkrat(b.q, b.p);
+        n = -n;
+    }
+    if (n > 64) {
+        if (b.p == 0 || (b.q == 1 && (b.p == 1 || b.p == -1))) {
+            if (b.p == 0) return Rat{0, 1};
+            return Rat{(b.p == -1 && (n & 1)) ? -1 : 1, 1};
+        }
+        throw Decline{};
+    }
+    Rat r{1, 1};
+    for (int64_t i = 0; i < n; ++i) r = rmul(r, b);
+    return r;
+}
+std::string rstr(Rat a) {
+    std::string s = std::to_string(a.p);
+    if (a.q != 1) s += "/" + std::to_string(a.q);
+    return s;
+}
+
+// ------------------------------------------------------------------ the expression DAG
+enum Kind : uint8_t { NUM, SYM, ADD, MUL, POW, EXP, ABS };
+
+struct Node {
+    Kind k;
+    Rat r;                 // NUM
+    int sym;               // SYM: index into the problem's symbol table
+    std::vector<int> a;    // children (ADD/MUL sorted by key; POW {base, exp}; EXP/ABS {arg})
+    std::string key;       // canonical form (also the hash-consing key)
+};
+
+struct SymInfo {
+    const char* name;
+    int coord;         // 0 = x (rho | r), 1 = y (z | x), -1 = constant
+    bool positive;     // SymPy assumptions (problems/__init__.py:70-71, :263-266)
+    Rat value;         // constants: the value KerrMagnetosphereValidator substitutes
+};
+
+const SymInfo kFFSyms[] = {{"rho", 0, true, {0, 1}}, {"z", 1, false, {0, 1}}};
+const SymInfo kKerrSyms[] = {{"r", 0, true, {0, 1}}, {"x", 1, false, {0, 1}},
+                             {"M", -1, true, {1, 1}}, {"a", -1, false, {1, 10}}};
+
+// three-valued logic for SymPy's assumption queries
+enum Tri : int8_t { NO = 0, YES = 1, UNK = 2 };
+
+struct Ctx {
+    const SymInfo* syms = nullptr;
+    int nsyms = 0;
+    // a deque: references to nodes stay valid while evaluation appends new ones
+    std::deque<Node> nodes;
+    std::unordered_map<std::string, int> intern;
+    int ZERO = -1, ONE = -1, NEG1 = -1;
+
+    void reset(const SymInfo* s, int n) {
+        syms = s;
+        nsyms = n;
+        nodes.clear();
+        intern.clear();
+        ZERO = num(Rat{0, 1});
+        ONE = num(Rat{1, 1});
+        NEG1 = num(Rat{-1, 1});
+    }
+    const Node& N(int i) const { return nodes[i]; }
+    int make(Node&& nd) {
+        auto it = intern.find(nd.key);
+        if (it != intern.end()) return it->second;
+        if (nodes.size() > 200000) throw Decline{};
+        const int id = (int)nodes.size();
+        intern.emplace(nd.key, id);
+        nodes.push_back(std::move(nd));
+        return id;
+    }
+    int num(Rat r) {
+        Node nd{NUM, r, -1, {}, rstr(r)};
+        return make(std::move(nd));
+    }
+    int sym(int s) {
+        Node nd{SYM, {}, s, {}, syms[s].name};
+        return make(std::move(nd));
+    }
+    // raw constructors (no evaluation): children are already canonical
+    int raw_nary(Kind k, std::vector<int> args) {
+        if (args.size() == 1) return args[0];
+        std::sort(args.begin(), args.end(), [&](int x, int y) { return nodes[x].key < nodes[y].key; });
+        std::string key = k == ADD ? "A(" : "M(";
+        for (size_t i = 0; i < args.size(); ++i) {
+            if (i) key += ",";
+            key += nodes[args[i]].key;
+        }
+        key += ")";
+        Node nd{k, {}, -1, std::move(args), std::move(key)};
+        return make(std::move(nd));
+    }
+    int raw_pow(int b, int e) {
+        std::string key = "P(" + nodes[b].key + "," + nodes[e].key + ")";
+        Node nd{POW, {}, -1, {b, e}, std::move(key)};
+        return make(std::move(nd));
+    }
+    int raw_fn(Kind k, int a) {
+        std::string key = std::string(k == EXP ? "E(" : "B(") + nodes[a].key + ")";
+        Node nd{k, {}, -1, {a}, std::move(key)};
+        return make(std::move(nd));
+    }
+    bool is_num(int i) const { return nodes[i].k == NUM; }
+    Rat rv(int i) const { return nodes[i].r; }
+
+    // ---------------------------------------------------------------- assumptions
+    // is_extended_real / is_extended_positive / is_extended_nonnegative /
+    // is_extended_negative / is_extended_nonpositive, restricted to this vocabulary
+    // zoo_ok: treat a negative power of a base that may be 0 as real (that is what
+    // re(b) >= 0 sees: re(1/z) = 1/z for a real z)
+    Tri real(int i, bool zoo_ok = false) {
+        const Node& n = nodes[i];
+        switch (n.k) {
+            case NUM: case SYM: case ABS: return YES;
+            case ADD: case MUL: {
+                for (int c : n.a) if (real(c) != YES) return UNK;
+                return YES;
+            }
+            case EXP: return real(n.a[0]) == YES ? YES : UNK;
+            case POW: {
+                const int b = n.a[0], e = n.a[1];
+                if (!is_num(e)) return UNK;
+                const Rat ex = rv(e);
+                // a negative power of a base that may be 0 may be zoo: not extended-real
+                if (ex.p < 0 && !zoo_ok && !nonzero(b)) return UNK;
+                if (rint(ex)) return real(b) == YES ? YES : UNK;
+                return nonneg(b) == YES ? YES : UNK;
+            }
+        }
+        return UNK;
+    }
+    // sign class: returns {positive, nonnegative, negative, nonpositive} as Tri each
+    struct Sign { Tri pos, nonneg, neg, nonpos; };
+    Sign sign(int i) {
+        const Node& n = nodes[i];
+        Sign u{UNK, UNK, UNK, UNK};
+        switch (n.k) {
+            case NUM: {
+                const int s = n.r.p > 0 ? 1 : (n.r.p < 0 ? -1 : 0);
+                return Sign{s > 0 ? YES : NO, s >= 0 ? YES : NO, s < 0 ? YES : NO, s <= 0 ? YES : NO};
+            }
+            case SYM:
+                if (syms[n.sym].positive) return Sign{YES, YES, NO, NO};
+                return u;
+            case ABS:
+                return Sign{UNK, YES, NO, UNK};
+            case EXP:
+                if (real(n.a[0]) == YES) return Sign{YES, YES, NO, NO};
+                return u;
+            case POW: {
+                const int b = n.a[0], e = n.a[1];
+                if (!is_num(e)) return u;
+                const Rat ex = rv(e);
+                const Sign sb = sign(b);
+                if (sb.pos == YES) return Sign{YES, YES, NO, NO};
+                if (ex.p < 0 && sb.neg != YES) {
+                    // b may be 0: only "not negative" survives for even powers
+                    if (rint(ex) && (ex.p % 2) == 0 && real(b) == YES) return Sign{UNK, UNK, NO, UNK};
+                    return u;
+                }
+                if (rint(ex)) {
+                    const bool even = (ex.p % 2) == 0;
+                    if (real(b) != YES) return u;
+                    if (even) {
+                        if (sb.neg == YES) return Sign{YES, YES, NO, NO};
+                        return Sign{UNK, YES, NO, UNK};
+                    }
+                    if (sb.neg == YES) return Sign{NO, NO, YES, YES};
+                    if (sb.nonneg == YES) return Sign{UNK, YES, NO, UNK};
+                    if (sb.nonpos == YES) return Sign{NO, UNK, UNK, YES};
+                    return u;
+                }
+                if (sb.nonneg == YES) return Sign{UNK, YES, NO, UNK};
+                return u;
+            }
+            case MUL: {
+                // Mul._eval_pos_neg: every factor's sign known (strict or not)
+                int s = 1;
+                bool weak = false;
+                for (int c : n.a) {
+                    const Sign sc = sign(c);
+                    if (sc.pos == YES) continue;
+                    if (sc.neg == YES) { s = -s; continue; }
+                    if (sc.nonneg == YES) { weak = true; continue; }
+                    if (sc.nonpos == YES) { s = -s; weak = true; continue; }
+                    return u;
+                }
+                if (s > 0) return weak ? Sign{UNK, YES, NO, UNK} : Sign{YES, YES, NO, NO};
+                return weak ? Sign{NO, UNK, UNK, YES} : Sign{NO, NO, YES, YES};
+            }
+            case ADD: {
+                bool all_nn = true, all_np = true, any_pos = false, any_neg = false;
+                for (int c : n.a) {
+                    const Sign sc = sign(c);
+                    if (sc.nonneg != YES) all_nn = false;
+                    if (sc.nonpos != YES) all_np = false;
+                    if (sc.pos == YES) any_pos = true;
+                    if (sc.neg == YES) any_neg = true;
+                }
+                if (all_nn) return any_pos ? Sign{YES, YES, NO, NO} : Sign{UNK, YES, NO, UNK};
+                if (all_np) return any_neg ? Sign{NO, NO, YES, YES} : Sign{NO, UNK, UNK, YES};
+                return u;
+            }
+        }
+        return u;
+    }
+    Tri nonneg(int i) { return sign(i).nonneg; }
+    bool nonzero(int i) { const Sign s = sign(i); return s.pos == YES || s.neg == YES; }
+
+    // as_coeff_Mul: (numeric coefficient, rest)
+    std::pair<Rat, int> coeff_mul(int i) {
+        const Node& n = nodes[i];
+        if (n.k == NUM) return {n.r, ONE};
+        if (n.k == MUL) {
+            // args are sorted by key, so the (single) numeric coefficient may sit anywhere
+            for (size_t j = 0; j < n.a.size(); ++j)
+                if (is_num(n.a[j])) {
+                    std::vector<int> rest;
+                    for (size_t k = 0; k < n.a.size(); ++k)
+                        if (k != j) rest.push_back(n.a[k]);
+                    return {rv(n.a[j]), raw_nary(MUL, rest)};
+                }
+        }
+        return {Rat{1, 1}, i};
+    }
+    // _keep_coeff(c, f) for a Rational c and a canonical f (no Add)
+    int keep_coeff(Rat c, int f) {
+        if (req(c, Rat{1, 1})) return f;
+        if (is_num(f)) return num(rmul(c, rv(f)));
+        auto cm = coeff_mul(f);
+        const Rat cc = rmul(c, cm.first);
+        if (req(cc, Rat{1, 1})) return cm.second;
+        if (cc.p == 0) return ZERO;
+        std::vector<int> args{num(cc)};
+        if (nodes[cm.second].k == MUL) {
+            for (int x : nodes[cm.second].a) args.push_back(x);
+        } else if (cm.second != ONE) {
+            args.push_back(cm.second);
+        }
+        return raw_nary(MUL, args);
+    }
+
+    // ---------------------------------------------------------------- Add (Add.flatten)
+    int add(const std::vector<int>& in) {
+        Rat coeff{0, 1};
+        std::vector<int> order;
+        std::unordered_map<int, Rat> terms;
+        std::vector<int> seq(in.begin(), in.end());
+        for (size_t i = 0; i < seq.size(); ++i) {
+            const int o = seq[i];
+            const Node& n = nodes[o];
+            if (n.k == NUM) { coeff = radd(coeff, n.r); continue; }
+            if (n.k == ADD) { for (int c : n.a) seq.push_back(c); continue; }
+            auto cm = (n.k == MUL) ? coeff_mul(o) : std::make_pair(Rat{1, 1}, o);
+            auto it = terms.find(cm.second);
+            if (it == terms.end()) { terms.emplace(cm.second, cm.first); order.push_back(cm.second); }
+            else it->second = radd(it->second, cm.first);
+        }
+        std::vector<int> out;
+        for (int s : order) {
+            const Rat c = terms[s];
+            if (c.p == 0) continue;
+            if (req(c, Rat{1, 1})) { out.push_back(s); continue; }
+            if (nodes[s].k == MUL) {
+                std::vector<int> args{num(c)};
+                for (int x : nodes[s].a) args.push_back(x);
+                out.push_back(raw_nary(MUL, args));
+            } else {
+                out.push_back(mul({num(c), s}));
+            }
+        }
+        if (coeff.p != 0) out.push_back(num(coeff));
+        if (out.empty()) return ZERO;
+        return raw_nary(ADD, out);
+    }
+
+    // ---------------------------------------------------------------- Mul (Mul.flatten)
+    struct BE { int base; Rat c; int term; };   // base ** (c * term); base -1 = E (exp)
+    // Mul(*in, *[Pow(b, e, evaluate=False) for (b, e) in pre]): `pre` are unevaluated powers,
+    // which Mul.flatten collects by their own base and re-evaluates in its rebuild
+    int mul(std::vector<int> in, const std::vector<BE>& pre = {}) {
+        in.erase(std::remove(in.begin(), in.end(), ONE), in.end());
+        if (pre.empty() && in.empty()) return ONE;
+        if (pre.empty() && in.size() == 1) return in[0];
+        if (pre.empty() && in.size() == 2) {
+            int a = in[0], b = in[1];
+            if (is_num(b) && !is_num(a)) std::swap(a, b);
+            if (is_num(a) && rv(a).p != 0 && nodes[b].k == ADD) {
+                // 2-arg Rational * Add distributes (Mul.flatten's 2-arg hack)
+                std::vector<int> ts;
+                for (int t : nodes[b].a) ts.push_back(keep_coeff(rv(a), t));
+                return add(ts);
+            }
+        }
+        Rat coeff{1, 1};
+        std::vector<BE> pw;
+        for (const BE& x : pre) {
+            if (is_num(x.base)) {   // Pow(Number, Integer) folds into the coefficient
+                if (!rint(x.c)) throw Decline{};
+                coeff = rmul(coeff, rpow_int(rv(x.base), x.c.p));
+            } else {
+                pw.push_back(x);
+            }
+        }
+        std::vector<int> seq(in.begin(), in.end());
+        for (size_t i = 0; i < seq.size(); ++i) {
+            const int o = seq[i];
+            const Node& n = nodes[o];
+            if (n.k == NUM) { coeff = rmul(coeff, n.r); continue; }
+            if (n.k == MUL) { for (int c : n.a) seq.push_back(c); continue; }
+            if (n.k == EXP) {
+                auto cm = coeff_mul(n.a[0]);
+                pw.push_back(BE{-1, cm.first, cm.second});
+                continue;
+            }
+            if (n.k == POW) {
+                if (!is_num(n.a[1])) throw Decline{};
+                if (is_num(n.a[0])) throw Decline{};   // numeric base with a rational power
+                pw.push_back(BE{n.a[0], rv(n.a[1]), ONE});
+                continue;
+            }
+            pw.push_back(BE{o, Rat{1, 1}, ONE});
+        }
+        if (coeff.p == 0) return ZERO;
+        std::vector<int> part;
+        for (int iter = 0; iter < 2; ++iter) {
+            // _gather: combine the coefficients of equal (base, term)
+            std::vector<BE> g;
+            for (const BE& x : pw) {
+                bool found = false;
+                for (BE& y : g)
+                    if (y.base == x.base && y.term == x.term) { y.c = radd(y.c, x.c); found = true; break; }
+                if (!found) g.push_back(x);
+            }
+            part.clear();
+            std::vector<BE> np;
+            bool changed = false;
+            for (const BE& x : g) {
+                if (x.c.p == 0) continue;
+                int p;
+                if (x.base < 0) {
+                    p = exp_(mul({num(x.c), x.term}));
+                    np.push_back(x);
+                } else if (req(x.c, Rat{1, 1}) && x.term == ONE) {
+                    p = x.base;
+                    np.push_back(x);
+                } else {
+                    p = pow_(x.base, num(x.c));
+                    if (nodes[p].k == POW && nodes[x.base].k != POW) {
+                        const int nb = nodes[p].a[0];
+                        if (nb != x.base) changed = true;
+                        np.push_back(BE{nb, is_num(nodes[p].a[1]) ? rv(nodes[p].a[1]) : Rat{1, 1}, ONE});
+                    } else {
+                        np.push_back(x);
+                    }
+                }
+                part.push_back(p);
+            }
+            bool dup = false;
+            for (size_t i = 0; i < np.size() && !dup; ++i)
+                for (size_t j = i + 1; j < np.size(); ++j)
+                    if (np[i].base == np[j].base) { dup = true; break; }
+            if (changed && dup) { pw = np; continue; }
+            break;
+        }
+        // the rebuilt powers may be numbers or products (Pow of a Mul base): fold them in
+        std::vector<int> fac;
+        for (int p : part) {
+            const Node& n = nodes[p];
+            if (n.k == NUM) coeff = rmul(coeff, n.r);
+            else fac.push_back(p);   // a product from Pow(b, e) stays one nested factor
+        }
+        if (coeff.p == 0) return ZERO;
+        if (fac.empty()) return num(coeff);
+        if (fac.size() == 1 && nodes[fac[0]].k == ADD && !req(coeff, Rat{1, 1})) {
+            std::vector<int> ts;
+            for (int t : nodes[fac[0]].a) ts.push_back(mul({num(coeff), t}));
+            return add(ts);
+        }
+        if (!req(coeff, Rat{1, 1})) fac.push_back(num(coeff));
+        return raw_nary(MUL, fac);
+    }
+
+    // ---------------------------------------------------------------- exp (exp.eval)
+    int exp_(int a) {
+        if (a == ZERO) return ONE;
+        return raw_fn(EXP, a);   // exp(1) is E: EXP(1) is how E is represented
+    }
+
+    // ---------------------------------------------------------------- Abs (Abs.eval)
+    // Expr.__neg__ / Mul.__neg__: an Add distributes (Mul(-1, Add)); a Mul flips its
+    // coefficient in place without re-flattening (nested products stay nested)
+    int neg(int a) {
+        const Node& n = nodes[a];
+        if (n.k == NUM) return num(rneg(n.r));
+        if (n.k == ADD) return mul({NEG1, a});
+        if (n.k == MUL) {
+            std::vector<int> args;
+            bool had = false;
+            for (int c : n.a) {
+                if (!had && is_num(c)) {
+                    had = true;
+                    const Rat nc = rneg(rv(c));
+                    if (!req(nc, Rat{1, 1})) args.push_back(num(nc));
+                } else {
+                    args.push_back(c);
+                }
+            }
+            if (!had) args.push_back(NEG1);
+            return raw_nary(MUL, args);
+        }
+        return raw_nary(MUL, {NEG1, a});
+    }
+    bool could_extract_minus(int i, bool* tie) {
+        // Add.could_extract_minus_sign: more terms with a minus sign than without
+        int negs = 0;
+        const Node& n = nodes[i];
+        for (int c : n.a) {
+            const Node& m = nodes[c];
+            if ((m.k == NUM && m.r.p < 0) || (m.k == MUL && coeff_mul(c).first.p < 0)) ++negs;
+        }
+        const int poss = (int)n.a.size() - negs;
+        *tie = negs == poss;
+        return negs > poss;
+    }
+    int abs_(int a) {
+        const Node& n = nodes[a];
+        if (n.k == NUM) return num(rabs(n.r));
+        if (n.k == ADD) {
+            if (has_nested_add(a)) throw Decline{};   // signsimp rewrites inner Adds
+            bool tie = false;
+            const bool flip = could_extract_minus(a, &tie);
+            if (tie) throw Decline{};       // SymPy breaks the tie by sort_key
+            if (flip) return abs_(neg(a));
+        }
+        if (n.k == MUL) {
+            // factor-wise (only when every factor is decided without an Abs; SymPy keeps the
+            // undecided ones under one unevaluated Abs)
+            if (has_nested_add(a)) throw Decline{};   // signsimp would rewrite them first
+            std::vector<int> known;
+            for (int c : n.a) {
+                const Node& cn = nodes[c];
+                if (cn.k == POW && is_num(cn.a[1]) && rint(rv(cn.a[1])) && rv(cn.a[1]).p < 0) {
+                    const int bnew = abs_(cn.a[0]);
+                    if (nodes[bnew].k == ABS) throw Decline{};
+                    known.push_back(pow_(bnew, cn.a[1]));
+                    continue;
+                }
+                const int t = abs_(c);
+                if (nodes[t].k == ABS) throw Decline{};
+                known.push_back(t);
+            }
+            return mul(known);
+        }
+        if (n.k == POW && is_num(n.a[1])) {
+            const int b = n.a[0];
+            const Rat e = rv(n.a[1]);
+            if (real(b) == YES) {
+                if (rint(e)) {
+                    if (e.p % 2 == 0) return a;
+                    return pow_(abs_(b), n.a[1]);
+                }
+                if (nonneg(b) == YES) return a;
+                throw Decline{};
+            }
+            throw Decline{};
+        }
+        if (n.k == EXP) {
+            if (real(n.a[0]) == YES) return a;
+            throw Decline{};
+        }
+        const Sign s = sign(a);
+        if ((s.nonneg == YES || s.nonpos == YES) && n.k == ADD && has_nested_add(a)) throw Decline{};
+        if (s.nonneg == YES) return a;
+        if (s.nonpos == YES) return neg(a);
+        if (n.k == SYM || (n.k == ADD && real(a) == YES)) return raw_fn(ABS, a);
+        throw Decline{};
+    }
+    // an Add strictly inside node i (SymPy's signsimp rewrites those before Abs.eval decides)
+    bool has_nested_add(int i) {
+        for (int c : nodes[i].a) {
+            if (nodes[c].k == ADD) return true;
+            if (has_nested_add(c)) return true;
+        }
+        return false;
+    }
+
+    // ---------------------------------------------------------------- Pow (Pow.__new__)
+    static bool half(Rat e) { return e.q == 2; }
+    int pow_(int b, int e) {
+        if (!is_num(e)) {
+            if (b == -2) return exp_(e);   // not used: E is declined at parse time
+            throw Decline{};               // symbolic exponents
+        }
+        const Rat ex = rv(e);
+        if (ex.p == 0) return ONE;
+        if (req(ex, Rat{1, 1})) return b;
+        const Node& bn = nodes[b];
+        if (bn.k == NUM) {
+            if (rint(ex)) return num(rpow_int(bn.r, ex.p));
+            if (req(bn.r, Rat{1, 1})) return ONE;
+            if (bn.r.p == 0 && ex.p > 0) return ZERO;
+            throw Decline{};     // irrational numeric power (sqrt(2) ...)
+        }
+        switch (bn.k) {
+            case EXP: {
+                // exp._eval_power -> Pow._eval_power(E**a, e): combine when e is an integer
+                // or a is real (E is positive)
+                const int a = bn.a[0];
+                if (rint(ex) || real(a) == YES) return exp_(mul({a, e}));
+                return raw_pow(b, e);
+            }
+            case POW: {
+                const int b1 = bn.a[0];
+                if (!is_num(bn.a[1])) throw Decline{};
+                const Rat e1 = rv(bn.a[1]);
+                if (rint(ex)) return pow_(b1, num(rmul(e1, ex)));
+                int bb = b1;
+                if (req(e1, Rat{-1, 1})) {
+                    if (half(ex)) {
+                        const Sign s = sign(b1);
+                        if (s.neg == YES) throw Decline{};
+                        if (s.neg == NO) return pow_(b1, num(rneg(ex)));
+                    }
+                } else if (rint(e1) && e1.p % 2 == 0) {
+                    if (real(b1) == YES) bb = abs_(b1);
+                }
+                bool s1 = false;
+                if (rcmp(rabs(e1), Rat{1, 1}) < 0 || req(e1, Rat{1, 1})) s1 = true;
+                else if (nonneg(bb) == YES) s1 = true;
+                if (s1) return pow_(bb, num(rmul(e1, ex)));
+                // re(b) >= 0 with |e1| < 2: for a real b that is the test above; for a b not
+                // known to be real SymPy may still decide re(b) (e.g. sqrt(z) + 1)
+                if (real(bb, true) != YES && rcmp(rabs(e1), Rat{2, 1}) < 0) throw Decline{};
+                if (half(ex) && sign(b1).neg == YES) throw Decline{};
+                return raw_pow(b, e);
+            }
+            case MUL: return pow_mul(b, e);
+            case ABS: {
+                // Abs._eval_power
+                const int a = bn.a[0];
+                if (real(a) == YES && rint(ex)) {
+                    if (ex.p % 2 == 0) return pow_(a, e);
+                    if (ex.p != -1) return mul({pow_(a, num(radd(ex, Rat{-1, 1}))), b});
+                }
+                return raw_pow(b, e);
+            }
+            default:
+                return raw_pow(b, e);
+        }
+    }
+    // Mul._eval_power + Pow._eval_expand_power_base(force=False)
+    int pow_mul(int b, int e) {
+        const Rat ex = rv(e);
+        const std::vector<int> args = nodes[b].a;
+        if (rint(ex)) {
+            // Mul(*[Pow(f, e, evaluate=False) for f in args])
+            std::vector<BE> pre;
+            for (int c : args) pre.push_back(BE{c, ex, ONE});
+            // ... * Pow(Mul._from_args(nc), e, evaluate=False): a second flatten, which
+            // merges the products the first one produced
+            return mul({mul({}, pre)}, {BE{ONE, ex, ONE}});
+        }
+        std::vector<int> nonneg_, negs, other;
+        for (int c : args) {
+            const Tri t = nonneg(c);
+            if (t == YES) nonneg_.push_back(c);
+            else if (t == NO) negs.push_back(c);
+            else other.push_back(c);
+        }
+        if (negs.size() > 1) {
+            // (-a)(-b)... : SymPy pulls the negatives out in pairs
+            throw Decline{};
+        } else if (!negs.empty() && !other.empty()) {
+            if (is_num(negs[0]) && negs[0] != NEG1) {
+                other.push_back(NEG1);
+                nonneg_.push_back(num(rneg(rv(negs[0]))));
+            } else {
+                other.insert(other.end(), negs.begin(), negs.end());
+            }
+        } else {
+            other.insert(other.end(), negs.begin(), negs.end());
+        }
+        for (int c : nonneg_)
+            if (is_num(c)) throw Decline{};   // numeric factor under a rational power
+        // rv = Mul(*[Pow(c, e, evaluate=False) for c in nonneg]); rv *= Pow(Mul(*other), e,
+        // evaluate=False)  (a one-factor Mul of an unevaluated Pow is that Pow itself)
+        std::vector<BE> pre;
+        for (int c : nonneg_) pre.push_back(BE{c, ex, ONE});
+        if (other.empty()) return pre.size() == 1 ? pow_(pre[0].base, e) : mul({}, pre);
+        const int ob = other.size() == 1 ? other[0] : mul(other);
+        if (pre.empty()) return other.size() == 1 ? pow_(ob, e) : raw_pow(b, e);
+        if (pre.size() == 1) {
+            pre.push_back(BE{ob, ex, ONE});
+            return mul({}, pre);
+        }
+        const int rv1 = mul({}, pre);
+        return mul({rv1}, {BE{ob, ex, ONE}});
+    }
+};
+
+// ------------------------------------------------------------------ parser
+struct Parser {
+    Ctx& C;
+    const char* s;
+    size_t n, i = 0;
+    Parser(Ctx& c, const char* str, size_t len) : C(c), s(str), n(len) {}
+
+    void ws() { while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) ++i; }
+    bool peek(char c) { ws(); return i < n && s[i] == c; }
+    bool peek2(const char* t) { ws(); return i + 1 < n && s[i] == t[0] && s[i + 1] == t[1]; }
+    void expect(char c) {
+        ws();
+        if (i >= n || s[i] != c) throw ParseError{};
+        ++i;
+    }
+    int parse() {
+        const int e = expr();
+        ws();
+        if (i != n) throw ParseError{};
+        return e;
+    }
+    // Python precedence: + -  <  * /  <  unary -  <  **
+    int expr() {
+        int acc = term();
+        for (;;) {
+            if (peek('+')) { ++i; acc = C.add({acc, term()}); }
+            else if (peek('-')) { ++i; acc = C.add({acc, C.neg(term())}); }
+            else return acc;
+        }
+    }
+    int term() {
+        int acc = unary();
+        for (;;) {
+            if (peek2("**")) return acc;   // cannot happen here (power binds tighter)
+            if (peek('*')) { ++i; acc = C.mul({acc, unary()}); }
+            else if (peek('/')) {
+                ++i;
+                if (peek('/')) throw Decline{};          // floor division
+                const int d = C.pow_(unary(), C.NEG1);
+                acc = (acc == C.ONE) ? d : C.mul({acc, d});
+            } else return acc;
+        }
+    }
+    int unary() {
+        if (peek('-')) { ++i; return C.neg(unary()); }
+        if (peek('+')) { ++i; return unary(); }
+        return power();
+    }
+    int power() {
+        const int b = atom();
+        if (peek2("**")) {
+            i += 2;
+            const int e = unary();       // right-assoc, exponent may carry a sign
+            return C.pow_(b, e);
+        }
+        return b;
+    }
+    int atom() {
+        ws();
+        if (i >= n) throw ParseError{};
+        const char c = s[i];
+        if (c == '(') {
+            ++i;
+            const int e = expr();
+            expect(')');
+            return e;
+        }
+        if (c >= '0' && c <= '9') {
+            const size_t st = i;
+            while (i < n && s[i] >= '0' && s[i] <= '9') ++i;
+            if (i < n && (s[i] == '.' || s[i] == 'e' || s[i] == 'E' || s[i] == 'j' || s[i] == '_'))
+                throw Decline{};         // Float / complex literals
+            if (i - st > 15) throw Decline{};
+            return C.num(Rat{(int64_t)strtoll(std::string(s + st, i - st).c_str(), nullptr, 10), 1});
+        }
+        if (c == '.') throw Decline{};
+        if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '_') {
+            const size_t st = i;
+            while (i < n && ((s[i] >= 'a' && s[i] <= 'z') || (s[i] >= 'A' && s[i] <= 'Z') ||
+                             (s[i] >= '0' && s[i] <= '9') || s[i] == '_'))
+                ++i;
+            const std::string name(s + st, i - st);
+            if (peek('(')) {
+                ++i;
+                const int a = expr();
+                if (peek(',')) throw Decline{};   // multi-argument functions
+                expect(')');
+                return call(name, a);
+            }
+            for (int k = 0; k < C.nsyms; ++k)
+                if (name == C.syms[k].name) return C.sym(k);
+            if (name == "E") return C.exp_(C.ONE);
+            throw Decline{};             // I, pi, zoo, oo, nan, unknown symbols
+        }
+        throw ParseError{};
+    }
+    // the sympify locals: UNARY_OPS of expression_operations.py:80-90 plus SymPy's own
+    int call(const std::string& f, int a) {
+        if (f == "neg") return C.neg(a);
+        if (f == "inv") return C.pow_(a, C.NEG1);
+        if (f == "sqrt") return C.pow_(a, C.num(Rat{1, 2}));
+        if (f == "square") return C.pow_(a, C.num(Rat{2, 1}));
+        if (f == "pow_3_2") return C.pow_(a, C.num(Rat{3, 2}));
+        if (f == "pow_neg_3_2") return C.pow_(a, C.num(Rat{-3, 2}));
+        if (f == "exp") return C.exp_(a);
+        if (f == "exp_neg") return C.exp_(C.neg(a));
+        if (f == "Abs") return C.abs_(a);
+        throw Decline{};                 // log, sin, undefined functions ...
+    }
+};
+
+// ------------------------------------------------------------------ lowering (flatten.py)
+// IR nodes as in flatten.py: x y c (neg sqrt exp log abs) pown pow (add sub mul div)
+enum IK : uint8_t { IX, IY, IC, INEG, ISQRT, IEXP, IABS, IPOWN, IPOW, IADD, ISUB, IMUL, IDIV };
+struct IR {
+    IK k;
+    double c = 0.0;   // IC value / IPOW exponent
+    bool irr = false; // IC: irrational constant (E), flatten.py's ('c', v, False)
+    Rat alpha;        // IPOW exact exponent (det_rational)
+    int n = 0;        // IPOWN
+    int a = -1, b = -1;
+};
+
+struct Lower {
+    Ctx& C;
+    std::vector<IR> ir;
+    explicit Lower(Ctx& c) : C(c) {}
+    int mk(IR x) { ir.push_back(x); return (int)ir.size() - 1; }
+    int cst(double v) { IR x{IC}; x.c = v; return mk(x); }
+    static double rdouble(Rat r) { return (double)r.p / (double)r.q; }   // exact p, q: correctly rounded
+    int un(IK k, int a) { IR x{k}; x.a = a; return mk(x); }
+    int bin(IK k, int a, int b) { IR x{k}; x.a = a; x.b = b; return mk(x); }
+    bool is_pvar(int i) const {
+        const IR& x = ir[i];
+        return x.k == IPOWN && (ir[x.a].k == IX || ir[x.a].k == IY) && x.n >= 2 && x.n <= 16;
+    }
+    bool is_leaf(int i) const { const IK k = ir[i].k; return k == IX || k == IY || k == IC || is_pvar(i); }
+    int need(int i) const {
+        const IR& x = ir[i];
+        switch (x.k) {
+            case IX: case IY: case IC: return 1;
+            case INEG: case ISQRT: case IEXP: case IABS: case IPOWN: case IPOW: return need(x.a);
+            default: break;
+        }
+        const int a = x.a, b = x.b;
+        if (is_leaf(b)) return need(a);
+        if ((is_leaf(a) && (x.k == IADD || x.k == IMUL || x.k == ISUB)) ||
+            (x.k == IDIV && (ir[a].k == IC || is_pvar(a))))
+            return need(b);
+        const int na = need(a), nb = need(b);
+        return na == nb ? na + 1 : std::max(na, nb);
+    }
+    int pown(int b, int n) {
+        if (n == 1) return b;
+        if (n <= 16) { IR x{IPOWN}; x.a = b; x.n = n; return mk(x); }
+        IR x{IPOW}; x.a = b; x.c = (double)n; x.alpha = Rat{n, 1}; return mk(x);
+    }
+    int node(int e) {
+        const Node& nd = C.N(e);
+        switch (nd.k) {
+            case SYM: {
+                const SymInfo& si = C.syms[nd.sym];
+                if (si.coord == 0) return mk(IR{IX});
+                if (si.coord == 1) return mk(IR{IY});
+                return cst(rdouble(si.value));
+            }
+            case NUM: return cst(rdouble(nd.r));
+            case ADD: return add(e);
+            case MUL: return mulnode(e);
+            case POW: return pownode(nd.a[0], nd.a[1]);
+            case EXP:
+                if (nd.a[0] == C.ONE) { IR x{IC}; x.c = 2.718281828459045; x.irr = true; return mk(x); }
+                return un(IEXP, node(nd.a[0]));
+            case ABS: return un(IABS, node(nd.a[0]));
+        }
+        throw Decline{};
+    }
+    // stable sort by key, like Python's list.sort
+    template <class T, class K> static void ssort(std::vector<T>& v, K key) {
+        std::stable_sort(v.begin(), v.end(), [&](const T& x, const T& y) { return key(x) < key(y); });
+    }
+    int add(int e) {
+        const Node& nd = C.N(e);
+        double cs = 0.0;
+        bool have = false;
+        std::vector<std::pair<int, int>> terms;   // (sign, ir)
+        for (int t : nd.a) {
+            if (C.is_num(t)) { cs += rdouble(C.rv(t)); have = true; continue; }
+            int sg = 1;
+            int tt = t;
+            if (C.N(t).k == MUL) {
+                auto cm = C.coeff_mul(t);
+                if (cm.first.p < 0) {
+                    sg = -1;
+                    const Rat pc = rneg(cm.first);
+                    tt = req(pc, Rat{1, 1}) ? cm.second : -1;
+                    if (tt < 0) {
+                        // Mul(-c, *rest, evaluate=False): lower with coefficient -c
+                        terms.push_back({sg, mulargs(cm.second, pc)});
+                        continue;
+                    }
+                }
+            }
+            terms.push_back({sg, node(tt)});
+        }
+        if (terms.empty()) return cst(cs);
+        ssort(terms, [&](const std::pair<int, int>& st) { return std::make_pair(st.first < 0 ? 1 : 0, -need(st.second)); });
+        int acc = terms[0].second;
+        if (terms[0].first < 0) acc = un(INEG, acc);
+        for (size_t k = 1; k < terms.size(); ++k)
+            acc = bin(terms[k].first > 0 ? IADD : ISUB, acc, terms[k].second);
+        if (have && cs != 0.0) acc = bin(IADD, acc, cst(cs));
+        return acc;
+    }
+    int mulnode(int e) { return mulargs(e, Rat{1, 1}); }
+    // flatten.py _Lower.mul over the factors of e (a Mul or a single factor) times coefficient
+    int mulargs(int e, Rat extra) {
+        std::vector<int> fs;
+        if (C.N(e).k == MUL) fs = C.N(e).a;
+        else if (e != C.ONE) fs.push_back(e);
+        double coef = 1.0;
+        bool first = true;
+        auto mulc = [&](Rat r) {
+            coef *= rdouble(r);
+            first = false;
+        };
+        if (!req(extra, Rat{1, 1})) mulc(extra);
+        std::vector<int> num, den;
+        for (int f : fs) {
+            const Node& fn = C.N(f);
+            if (fn.k == NUM) { mulc(fn.r); continue; }
+            if (fn.k == POW && C.is_num(fn.a[1]) && rint(C.rv(fn.a[1])) && C.rv(fn.a[1]).p < 0) {
+                const int64_t n = -C.rv(fn.a[1]).p;
+                const int b = node(fn.a[0]);
+                den.push_back(n == 1 ? b : pown(b, (int)n));
+                continue;
+            }
+            num.push_back(node(f));
+        }
+        (void)first;
+        ssort(num, [&](int x) { return -need(x); });
+        ssort(den, [&](int x) { return -need(x); });
+        auto product = [&](const std::vector<int>& v) {
+            int acc = v[0];
+            for (size_t k = 1; k < v.size(); ++k) acc = bin(IMUL, acc, v[k]);
+            return acc;
+        };
+        if (!num.empty()) {
+            int acc = product(num);
+            if (!den.empty()) acc = bin(IDIV, acc, product(den));
+            if (coef == -1.0) acc = un(INEG, acc);
+            else if (coef != 1.0) acc = bin(IMUL, acc, cst(coef));
+            return acc;
+        }
+        if (!den.empty()) return bin(IDIV, cst(coef), product(den));
+        return cst(coef);
+    }
+    int pownode(int base, int ex) {
+        if (!C.is_num(ex)) throw Decline{};
+        const Rat e = C.rv(ex);
+        if (rint(e)) {
+            if (e.p == 0) return cst(1.0);
+            const int b = node(base);
+            if (e.p > 0) return pown(b, (int)std::min<int64_t>(e.p, 1 << 20));
+            return bin(IDIV, cst(1.0), pown(b, (int)std::min<int64_t>(-e.p, 1 << 20)));
+        }
+        const int b = node(base);
+        if (req(e, Rat{1, 2})) return un(ISQRT, b);
+        IR x{IPOW};
+        x.a = b;
+        x.c = rdouble(e);
+        x.alpha = e;
+        return mk(x);
+    }
+
+    // ---- det_rational (flatten.py _det_kind / det_rational)
+    struct Kd {
+        int t;                    // 0 = None, 1 = 'R', 2 = 'C', 3 = ('P', exps, pure)
+        std::vector<Rat> ex;
+        bool pure = false;
+    };
+    Kd kind(int i) {
+        const IR& x = ir[i];
+        switch (x.k) {
+            case IX: case IY: return Kd{1, {}, false};
+            case IC: return Kd{x.irr ? 2 : 1, {}, false};
+            case INEG: case IABS: return kind(x.a);
+            case IEXP: { Kd k = kind(x.a); return k.t == 2 ? Kd{2, {}, false} : Kd{0, {}, false}; }
+            case ISQRT: case IPOWN: case IPOW: {
+                const Rat e = x.k == ISQRT ? Rat{1, 2} : (x.k == IPOWN ? Rat{x.n, 1} : x.alpha);
+                Kd k = kind(x.a);
+                if (k.t == 2) return Kd{2, {}, false};
+                if (k.t == 1) {
+                    if (rint(e)) return Kd{1, {}, false};
+                    return Kd{3, {e}, true};
+                }
+                if (k.t == 3 && k.pure) {
+                    std::vector<Rat> ex;
+                    for (Rat a : k.ex) { Rat m = rmul(a, e); if (!rint(m)) ex.push_back(m); }
+                    if (ex.empty()) return Kd{1, {}, false};
+                    return Kd{3, ex, true};
+                }
+                return Kd{0, {}, false};
+            }
+            default: break;
+        }
+        const int a = x.a, b = x.b;
+        Kd ka = kind(a), kb = kind(b);
+        if (x.k == IADD || x.k == ISUB) {
+            if (ka.t == kb.t && (ka.t == 1 || ka.t == 2)) return Kd{ka.t, {}, false};
+            if (((ka.t == 1 && kb.t == 2) || (ka.t == 2 && kb.t == 1)) &&
+                ((ka.t == 1 && ir[a].k == IC) || (kb.t == 1 && ir[b].k == IC)))
+                return Kd{2, {}, false};
+            return Kd{0, {}, false};
+        }
+        if (ka.t == 0 || kb.t == 0 || ka.t == 2 || kb.t == 2) return Kd{0, {}, false};
+        if (ka.t == 1 && kb.t == 1) return Kd{1, {}, false};
+        std::vector<Rat> ex = ka.t == 3 ? ka.ex : std::vector<Rat>{};
+        if (kb.t == 3)
+            for (Rat r : kb.ex) ex.push_back(x.k == IDIV ? rneg(r) : r);
+        const bool pa = (ka.t == 1 && ir[a].k == IC) || (ka.t == 3 && ka.pure);
+        const bool pb = (kb.t == 1 && ir[b].k == IC) || (kb.t == 3 && kb.pure);
+        return Kd{3, ex, pa && pb};
+    }
+    bool det_rational(int root) {
+        int n = root;
+        for (;;) {
+            const IR& x = ir[n];
+            if (x.k == INEG) { n = x.a; continue; }
+            if (x.k == IADD || x.k == ISUB) {
+                if (ir[x.a].k == IC || kind(x.a).t == 2) { n = x.b; continue; }
+                if (ir[x.b].k == IC || kind(x.b).t == 2) { n = x.a; continue; }
+            } else if (x.k == IMUL && ir[x.a].k == IC && !ir[x.a].irr) { n = x.b; continue; }
+            else if ((x.k == IMUL || x.k == IDIV) && ir[x.b].k == IC && !ir[x.b].irr) { n = x.a; continue; }
+            break;
+        }
+        Kd k = kind(n);
+        if (k.t == 1 || k.t == 2) return true;
+        if (k.t != 3) return false;
+        for (Rat r : k.ex) if (!rint(rmul(r, Rat{6, 1}))) return false;
+        return true;
+    }
+};
+
+// ------------------------------------------------------------------ emission (flatten.py _Emit)
+struct Emit {
+    const Lower& L;
+    std::vector<int32_t> w;
+    int d = 0, dmax = 0;
+    explicit Emit(const Lower& l) : L(l) {}
+    void op(int code, int arg = 0) {
+        w.push_back(code | (arg << 8));
+        if (code == PDOP_PUSH_X || code == PDOP_PUSH_Y || code == PDOP_PUSH_C || code == PDOP_PUSH_P) {
+            ++d;
+            dmax = std::max(dmax, d);
+        } else if (code == PDOP_ADD || code == PDOP_SUB || code == PDOP_RSUB || code == PDOP_MUL ||
+                   code == PDOP_DIV || code == PDOP_RDIV) {
+            --d;
+        }
+    }
+    void opi(int code, double imm) {
+        op(code);
+        uint64_t u;
+        memcpy(&u, &imm, 8);
+        w.push_back((int32_t)(uint32_t)(u & 0xffffffffu));
+        w.push_back((int32_t)(uint32_t)(u >> 32));
+    }
+    int parg(int i) const { return L.ir[i].n | ((L.ir[L.ir[i].a].k == IX ? 0 : 1) << 8); }
+    void leaf(int i) {
+        const IR& x = L.ir[i];
+        if (L.is_pvar(i)) op(PDOP_PUSH_P, parg(i));
+        else if (x.k == IX) op(PDOP_PUSH_X);
+        else if (x.k == IY) op(PDOP_PUSH_Y);
+        else opi(PDOP_PUSH_C, x.c);
+    }
+    void fused(IK k, int lf) {
+        const IR& x = L.ir[lf];
+        if (L.is_pvar(lf)) {
+            op(k == IADD ? PDOP_ADD_P : k == ISUB ? PDOP_SUB_P : k == IMUL ? PDOP_MUL_P : PDOP_DIV_P, parg(lf));
+            return;
+        }
+        if (x.k == IC) {
+            const double c = x.c;
+            if (k == IADD) opi(PDOP_ADDC, c);
+            else if (k == ISUB) opi(PDOP_ADDC, -c);
+            else if (k == IMUL) { if (c == -1.0) op(PDOP_NEG); else opi(PDOP_MULC, c); }
+            else opi(PDOP_MULC, 1.0 / c);
+            return;
+        }
+        const bool isx = x.k == IX;
+        if (k == IADD) op(isx ? PDOP_ADD_X : PDOP_ADD_Y);
+        else if (k == ISUB) op(isx ? PDOP_SUB_X : PDOP_SUB_Y);
+        else if (k == IMUL) op(isx ? PDOP_MUL_X : PDOP_MUL_Y);
+        else op(isx ? PDOP_DIV_X : PDOP_DIV_Y);
+    }
+    void emit(int i) {
+        const IR& x = L.ir[i];
+        if (x.k == IX || x.k == IY || x.k == IC || L.is_pvar(i)) { leaf(i); return; }
+        switch (x.k) {
+            case INEG: emit(x.a); op(PDOP_NEG); return;
+            case ISQRT: emit(x.a); op(PDOP_SQRT); return;
+            case IEXP: emit(x.a); op(PDOP_EXP); return;
+            case IABS: emit(x.a); op(PDOP_ABS); return;
+            case IPOWN: emit(x.a); op(PDOP_POWN, x.n); return;
+            case IPOW: emit(x.a); opi(PDOP_POW, x.c); return;
+            default: break;
+        }
+        const int a = x.a, b = x.b;
+        const IK k = x.k;
+        if (L.is_leaf(b)) { emit(a); fused(k, b); return; }
+        if (L.is_leaf(a) && (k == IADD || k == IMUL)) { emit(b); fused(k, a); return; }
+        if (L.is_leaf(a) && k == ISUB) { emit(b); op(PDOP_NEG); fused(IADD, a); return; }
+        if (k == IDIV && L.ir[a].k == IC) { emit(b); opi(PDOP_RDIVC, L.ir[a].c); return; }
+        if (k == IDIV && L.is_pvar(a)) { emit(b); op(PDOP_RDIV_P, parg(a)); return; }
+        const int na = L.need(a), nb = L.need(b);
+        static const int fwd[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, PDOP_ADD, PDOP_SUB, PDOP_MUL, PDOP_DIV};
+        static const int rev[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, PDOP_ADD, PDOP_RSUB, PDOP_MUL, PDOP_RDIV};
+        if (na >= nb) { emit(a); emit(b); op(fwd[k]); }
+        else { emit(b); emit(a); op(rev[k]); }
+    }
+};
+
+bool is_p_op(int o) { return o >= PDOP_PUSH_P && o <= PDOP_RDIV_P; }
+
+// compile one string; returns 0 (compiled), 1 (declined), 2 (parse error)
+int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t len,
+                std::vector<int32_t>& out, std::string* canon) {
+    try {
+        C.reset(syms, nsyms);
+        Parser P(C, s, len);
+        const int root = P.parse();
+        if (canon) *canon = C.N(root).key;
+        Lower L(C);
+        const int ir = L.node(root);
+        Emit E(L);
+        E.emit(ir);
+        if (E.d != 1) return 2;
+        if (E.dmax > PDEVAL_MAX_STACK) throw Decline{};   // the SymPy path reports it
+        bool xs = false, ys = false, ab = false;
+        for (size_t k = 0; k < E.w.size();) {
+            const int o = E.w[k] & 0xff;
+            const uint32_t wd = (uint32_t)E.w[k];
+            if (o == PDOP_PUSH_X || o == PDOP_ADD_X || o == PDOP_SUB_X || o == PDOP_MUL_X || o == PDOP_DIV_X) xs = true;
+            if (o == PDOP_PUSH_Y || o == PDOP_ADD_Y || o == PDOP_SUB_Y || o == PDOP_MUL_Y || o == PDOP_DIV_Y) ys = true;
+            if (is_p_op(o)) { if ((wd >> 16) & 1) ys = true; else xs = true; }
+            if (o == PDOP_ABS) ab = true;
+            k += (o == PDOP_PUSH_C || o == PDOP_ADDC || o == PDOP_MULC || o == PDOP_RDIVC || o == PDOP_POW) ? 3 : 1;
+        }
+        uint32_t hdr = (uint32_t)(E.dmax << 8);
+        if (!(xs || ys)) hdr |= PDEVAL_FLAG_NOCOORD;
+        if (L.det_rational(ir)) hdr |= PDEVAL_FLAG_RATIONAL;
+        if (xs && ys && ab) hdr |= PDEVAL_FLAG_NONSMOOTH2D;
+        out.clear();
+        out.push_back((int32_t)hdr);
+        out.insert(out.end(), E.w.begin(), E.w.end());
+        return 0;
+    } catch (const Decline&) {
+        return 1;
+    } catch (const ParseError&) {
+        return 2;
+    }
+}
+
+bool problem_syms(int problem_id, const SymInfo** s, int* n) {
+    if (problem_id == PDEVAL_PROBLEM_FORCE_FREE) { *s = kFFSyms; *n = 2; return true; }
+    if (problem_id == PDEVAL_PROBLEM_KERR) { *s = kKerrSyms; *n = 4; return true; }
+    return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pdeval_compile_batch(int problem_id, const char* text, const int64_t* str_offsets, int64_t n,
+                         int32_t* ops, int64_t ops_cap, int64_t* offsets, int32_t* status,
+                         int64_t* n_words_out) {
+    const SymInfo* syms;
+    int nsyms;
+    if (!problem_syms(problem_id, &syms, &nsyms) || n < 0 || (n > 0 && (!text || !str_offsets)) ||
+        !offsets || !status)
+        return PDEVAL_ERR_ARG;
+    Ctx C;
+    std::vector<int32_t> prog;
+    int64_t pos = 0;
+    offsets[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t b = str_offsets[i], e = str_offsets[i + 1];
+        if (b < 0 || e < b) return PDEVAL_ERR_ARG;
+        int st = compile_one(C, syms, nsyms, text + b, (size_t)(e - b), prog, nullptr);
+        if (st == 0 && pos + (int64_t)prog.size() > ops_cap) {
+            if (n_words_out) *n_words_out = -1;   // buffer too small
+            return PDEVAL_ERR_ARG;
+        }
+        if (st == 0) {
+            memcpy(ops + pos, prog.data(), prog.size() * sizeof(int32_t));
+            pos += (int64_t)prog.size();
+        }
+        status[i] = st;
+        offsets[i + 1] = pos;   // declined / unparsable strings get an empty slot
+    }
+    if (n_words_out) *n_words_out = pos;
+    return PDEVAL_OK;
+}
+
+int pdeval_canonical(int problem_id, const char* s, int64_t len, char* out, int64_t cap) {
+    const SymInfo* syms;
+    int nsyms;
+    if (!problem_syms(problem_id, &syms, &nsyms) || !s || len < 0 || !out || cap <= 0) return -1;
+    Ctx C;
+    std::vector<int32_t> prog;
+    std::string canon;
+    const int st = compile_one(C, syms, nsyms, s, (size_t)len, prog, &canon);
+    if (st != 0) { out[0] = 0; return st; }
+    if ((int64_t)canon.size() + 1 > cap) return -1;
+    memcpy(out, canon.c_str(), canon.size() + 1);
+    return 0;
+}
+
+}  // extern "C"

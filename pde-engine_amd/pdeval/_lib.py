@@ -23,6 +23,7 @@ EXPORTS = (
     'pdeval_n_points', 'pdeval_default_params', 'pdeval_validate_batch',
     'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
     'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts', 'pdeval_eval_points',
+    'pdeval_compile_batch', 'pdeval_canonical',
 )
 LIST_NAMES = ('defer_stack3', 'complex', 'defer_stack8', 'tier2', 'tier2_stack3', 'tier2_complex',
               'complex_stack8', 'tier2_stack8')
@@ -77,6 +78,8 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_pass_times.argtypes = [vp, vp, C.c_int, vp]
     lib.pdeval_pass_counts.argtypes = [vp, vp, C.c_int]
     lib.pdeval_eval_points.argtypes = [vp, vp, i64, vp, vp, C.c_int, C.c_int, vp, vp]
+    lib.pdeval_compile_batch.argtypes = [C.c_int, vp, vp, i64, vp, i64, vp, vp, vp]
+    lib.pdeval_canonical.argtypes = [C.c_int, C.c_char_p, i64, C.c_char_p, i64]
     for name in EXPORTS:
         getattr(lib, name)   # every symbol of the header must resolve
     if path is None:

@@ -176,3 +176,22 @@ def test_ff_point_arithmetic(ff_ctx, s):
         if not ok:
             bad.append((xs[i], ys[i], d.tolist(), o.tolist()))
     assert len(bad) <= 2, (len(bad), bad[:5])   # 2 of 4097: exact-boundary overflow cases
+
+
+def test_native_compile_full_d4(ff_ctx):
+    """All 142,004 validated force-free depth-4 strings: programs from the native compiler
+    (csrc/pdcompile.cpp; SymPy only for the strings it declines) get the same class on the
+    device as the SymPy-compiled programs of data/force_free_d4_validated.npz."""
+    import os
+    from pdeval import native
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             'data', 'force_free_d4_validated.npz'))
+    strings = [str(s) for s in d['exprs']]
+    ops, off, st = native.compile_native(0, strings)
+    ok = np.flatnonzero(st == native.COMPILE_OK)
+    assert len(ok) >= 0.97 * len(strings)
+    nat = ff_ctx.validate(ops, off)                    # declined strings: empty -> BAD_PROGRAM
+    ref = ff_ctx.validate(d['ops'], d['offsets'])
+    diff = ok[nat['status'][ok] != ref['status'][ok]]
+    assert not diff.size, [(strings[i], int(nat['status'][i]), int(ref['status'][i])) for i in diff[:10]]
+    assert np.array_equal(nat['verdict'][ok], ref['verdict'][ok])

@@ -1,0 +1,141 @@
+"""CPU tests: the native candidate compiler (csrc/pdcompile.cpp, C ABI pdeval_compile_batch)
+against SymPy, which is what the reference parses with (``sp.sympify(s, locals=...)``,
+general_method_paper_reproduction.py:84-93, :1767).
+
+* structure: for every string it compiles, the canonical form of its evaluated tree equals that
+  of sympify's tree (same Add/Mul/Pow/exp/Abs nodes, same exact rationals), on the committed
+  candidate streams (all of force-free d<=3, a seeded sample of d4 and of Kerr d<=3);
+* programs: header flags (NOCOORD, RATIONAL, NONSMOOTH2D, COMPLEX) equal flatten.py's;
+* verdicts: the hybrid compile (native, SymPy for declined strings) gives the oracle the same
+  class as the SymPy path on every reference fixture, and the reference's verdict;
+* the declined share stays small (those strings cost what they cost today).
+The full streams (142,004 d4 strings) are checked by scripts/native_parity.py and on the GPU by
+tests/test_gpu_parity.py::test_native_compile_full_d4.
+"""
+import gzip
+import os
+import random
+
+import numpy as np
+import pytest
+
+import golden_data as G
+import oracle_lib as O
+from pdeval import native
+from pdeval import problem_defs as P
+from pdeval.batch import reason_for
+from pdeval.opcodes import FLAG_RATIONAL
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STREAMS = os.path.join(ROOT, 'tests', 'golden', 'streams')
+DEPTH_MASK = ~0xff00   # the stack depth may differ (argument order of equal-need terms)
+
+
+def _stream(name):
+    with gzip.open(os.path.join(STREAMS, name), 'rt') as f:
+        return [line.rstrip('\n').split('\t')[-1] for line in f]
+
+
+def _sample(xs, k, seed=0):
+    if len(xs) <= k:
+        return xs
+    return random.Random(seed).sample(xs, k)
+
+
+def _check_structure(prob, strings, max_declined):
+    pd_ = P.get(prob)
+    ops, off, st = native.compile_native(pd_.problem_id, strings)
+    bad = []
+    for i, s in enumerate(strings):
+        if st[i] != native.COMPILE_OK:
+            continue
+        _, cn = native.canonical(pd_.problem_id, s)
+        e = pd_.parse(s)
+        cs = native.sympy_canonical(e)
+        if cn != cs:
+            bad.append((s, cn, cs))
+            continue
+        w = pd_.compile(e)
+        if (int(ops[off[i]]) & DEPTH_MASK) != (w[0] & DEPTH_MASK):
+            bad.append((s, hex(int(ops[off[i]])), hex(w[0])))
+    assert not bad, bad[:10]
+    declined = int((st != native.COMPILE_OK).sum())
+    assert declined <= max_declined * len(strings), declined
+    return declined
+
+
+def test_structure_force_free_d3_all():
+    _check_structure('force_free', _stream('force_free_d3_validated.txt.gz'), 0.02)
+
+
+def test_structure_force_free_d4_sample():
+    _check_structure('force_free', _sample(_stream('force_free_d4_validated.txt.gz'), 3000), 0.03)
+
+
+def test_structure_kerr_d3_sample():
+    _check_structure('kerr', _sample(_stream('kerr_magnetosphere_d3_validated.txt.gz'), 2000), 0.03)
+
+
+# constructs whose SymPy evaluation depends on assumptions or on nested-power rules
+EDGE = ['sqrt(rho**2/z**2)', 'sqrt(z**2)', 'pow_3_2(square(z))', '(z**(3/2))**(3/2)',
+        '(rho**(3/2))**(3/2)', 'sqrt(exp(z))', 'sqrt(exp(rho/z))', 'exp(z)/exp(z)**2',
+        '(rho*z)**(3/2)', '(-z)**(1/2)', '-(rho+z)', '2*(rho+z)/3', '(rho+z)*2*rho',
+        'rho**2 - rho + z**2 - square(rho)', 'neg(z)/z', 'inv(rho/z)', '(1/z)**(1/2)',
+        'sqrt(1/rho)', 'pow_neg_3_2(1/z)', 'square(pow_3_2(square(z)))',
+        'inv(pow_3_2(square(rho/z)))', 'neg(pow_3_2(square(rho/z)))', 'square(sqrt(neg(rho/z)))',
+        'E*exp(rho)', 'exp(-1)*exp(rho)', 'Abs(-rho-1)', 'Abs(rho*z)', 'exp(rho+z)**2',
+        'z**(1/2)*z**(3/2)*rho', 'rho/(2*(rho+z))', '1/(1/z)', 'sqrt((rho-z)**2)',
+        '(z**2*(rho+z))**(1/2)', 'rho**2*exp(-2*z)', 'sqrt(z**2 + (rho - 1)**2) - sqrt(z**2 + (rho + 1)**2)']
+
+
+@pytest.mark.parametrize('s', EDGE)
+def test_edge_structure(s):
+    pd_ = P.force_free()
+    st, cn = native.canonical(pd_.problem_id, s)
+    if st != native.COMPILE_OK:
+        pytest.skip('declined (compiled through SymPy)')
+    assert cn == native.sympy_canonical(pd_.parse(s))
+
+
+def test_parse_errors_and_declines():
+    pd_ = P.force_free()
+    ops, off, st = native.compile_native(pd_.problem_id, ['rho +', 'log(rho)', '1.5*rho', 'I*z', 'rho'])
+    assert list(st) == [native.COMPILE_PARSE, native.COMPILE_DECLINED, native.COMPILE_DECLINED,
+                        native.COMPILE_DECLINED, native.COMPILE_OK]
+    assert off[4] == off[0] and off[5] > off[4]
+
+
+def test_hybrid_equals_sympy_programs_where_identical():
+    """The splice of native and SymPy-compiled programs keeps every candidate in place."""
+    pd_ = P.force_free()
+    strings = ['rho', 'log(rho)', 'rho**2*z', '1.5*rho', 'sqrt(2)*sqrt(z)', 'exp(rho*z)']
+    ops, off, notes = native.compile_strings(pd_, strings)
+    s_ops, s_off, _ = P.compile_strings(pd_, strings)
+    for i in range(len(strings)):
+        a = ops[off[i]:off[i + 1]]
+        b = s_ops[s_off[i]:s_off[i + 1]]
+        assert (a[0] & DEPTH_MASK) == (b[0] & DEPTH_MASK), strings[i]
+    for i in (1, 3, 4):   # declined: compiled by SymPy, so identical
+        assert np.array_equal(ops[off[i]:off[i + 1]], s_ops[s_off[i]:s_off[i + 1]])
+
+
+@pytest.mark.parametrize('prob,files', [('force_free', G.FF_REF + ('ff_edge.jsonl',)),
+                                        ('kerr', G.KERR_REF + ('kerr_edge.jsonl',))])
+def test_native_verdicts_match_reference_and_sympy_path(prob, files):
+    pd_ = P.get(prob)
+    rows = G.decided(G.ref_rows(*files))
+    strings = [r['expr'] for r in rows]
+    ops, off, notes = native.compile_strings(pd_, strings)
+    s_ops, s_off, _ = P.compile_strings(pd_, strings)
+    res = O.validate(pd_.problem_id, ops, off)
+    ref = O.validate(pd_.problem_id, s_ops, s_off)
+    assert np.array_equal(res['status'], ref['status']), \
+        [(strings[i], int(res['status'][i]), int(ref['status'][i]))
+         for i in np.flatnonzero(res['status'] != ref['status'])[:10]]
+    bad = []
+    for i, r in enumerate(rows):
+        ok, _ = reason_for(pd_.problem_id, int(res['status'][i]), res['res_ref'][i], res['q_ref'][i],
+                           res['q_grid'][i], bool(int(ops[off[i]]) & FLAG_RATIONAL), notes[i])
+        if ok != r['ok']:
+            bad.append((r['expr'], r['reason']))
+    assert not bad, bad[:10]
