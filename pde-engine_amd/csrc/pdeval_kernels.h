@@ -314,7 +314,8 @@ template <class T, int K> struct JetOps {
         set_const(a, c);
         div(a, t);
     }
-    // t = t*t with the symmetric half of the products
+    // t = t*t with the symmetric half of the products (into a temporary: computing it in place
+    // was measured to raise pass 1's scratch from 64 to 80 bytes per lane)
     static PD_HD void square(J& t) {
         J r;
 #pragma unroll
@@ -767,6 +768,9 @@ void validate_kernel(KernelArgs a) {
     static unsigned char pd_lds[1];
 #endif
     T* stk = reinterpret_cast<T*>(pd_lds) + (size_t)wib * (MAXD - 1) * nc(K) * 64;
+    // (An XCD-contiguous block renumbering was measured here and rejected: pass 1 went from
+    // 132.9 to 134.9 ms and its write traffic is dominated by scratch, not by partial lines of
+    // the per-candidate outputs -- DESIGN.md §7.)
     const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
     // persistent variants stride over a device work list; the first pass is one wave per
     // candidate (a single iteration)

@@ -187,10 +187,11 @@ def test_native_compile_full_d4(ff_ctx):
     d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                              'data', 'force_free_d4_validated.npz'))
     strings = [str(s) for s in d['exprs']]
-    ops, off, st = native.compile_native(0, strings)
+    _, _, st = native.compile_native(0, strings)
     ok = np.flatnonzero(st == native.COMPILE_OK)
     assert len(ok) >= 0.97 * len(strings)
-    nat = ff_ctx.validate(ops, off)                    # declined strings: empty -> BAD_PROGRAM
+    ops, off, _ = native.compile_strings(P.force_free(), strings)   # declined: through SymPy
+    nat = ff_ctx.validate(ops, off)
     ref = ff_ctx.validate(d['ops'], d['offsets'])
     diff = ok[nat['status'][ok] != ref['status'][ok]]
     assert not diff.size, [(strings[i], int(nat['status'][i]), int(ref['status'][i])) for i in diff[:10]]
