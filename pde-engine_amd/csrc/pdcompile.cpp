@@ -185,17 +185,17 @@ struct Ctx {
         switch (n.k) {
             case NUM: case SYM: case ABS: return YES;
             case ADD: case MUL: {
-                for (int c : n.a) if (real(c) != YES) return UNK;
+                for (int c : n.a) if (real(c, zoo_ok) != YES) return UNK;
                 return YES;
             }
-            case EXP: return real(n.a[0]) == YES ? YES : UNK;
+            case EXP: return real(n.a[0], zoo_ok) == YES ? YES : UNK;
             case POW: {
                 const int b = n.a[0], e = n.a[1];
                 if (!is_num(e)) return UNK;
                 const Rat ex = rv(e);
                 // a negative power of a base that may be 0 may be zoo: not extended-real
                 if (ex.p < 0 && !zoo_ok && !nonzero(b)) return UNK;
-                if (rint(ex)) return real(b) == YES ? YES : UNK;
+                if (rint(ex)) return real(b, zoo_ok) == YES ? YES : UNK;
                 return nonneg(b) == YES ? YES : UNK;
             }
         }
@@ -548,6 +548,14 @@ struct Ctx {
         if (n.k == SYM || (n.k == ADD && real(a) == YES)) return raw_fn(ABS, a);
         throw Decline{};
     }
+    // an exp(a) inside node i whose argument is not known to be real (only real-or-zoo)
+    bool has_weak_exp(int i) {
+        const Node& n = nodes[i];
+        if (n.k == EXP && real(n.a[0]) != YES) return true;
+        for (int c : n.a)
+            if (has_weak_exp(c)) return true;
+        return false;
+    }
     // an Add strictly inside node i (SymPy's signsimp rewrites those before Abs.eval decides)
     bool has_nested_add(int i) {
         for (int c : nodes[i].a) {
@@ -603,7 +611,14 @@ struct Ctx {
                 if (s1) return pow_(bb, num(rmul(e1, ex)));
                 // re(b) >= 0 with |e1| < 2: for a real b that is the test above; for a b not
                 // known to be real SymPy may still decide re(b) (e.g. sqrt(z) + 1)
-                if (real(bb, true) != YES && rcmp(rabs(e1), Rat{2, 1}) < 0) throw Decline{};
+                if (rcmp(rabs(e1), Rat{2, 1}) < 0) {
+                    if (real(bb, true) != YES) throw Decline{};
+                    // a real-or-zoo b: re(b) is b itself, except through exp of an argument
+                    // that may be zoo, where re(exp(a)) = exp(re(a)) is decided positive
+                    if (nodes[bb].k == EXP && real(nodes[bb].a[0]) != YES)
+                        return pow_(bb, num(rmul(e1, ex)));
+                    if (has_weak_exp(bb)) throw Decline{};
+                }
                 if (half(ex) && sign(b1).neg == YES) throw Decline{};
                 return raw_pow(b, e);
             }
