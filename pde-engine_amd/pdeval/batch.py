@@ -112,9 +112,12 @@ class BatchValidator:
         if not exprs:
             return []
         ops, off, notes = self.compile(exprs)
+        return self._verdicts(ops, off, notes)
+
+    def _verdicts(self, ops, off, notes) -> List[Verdict]:
         r = self.run(ops, off)
         out = []
-        for i in range(len(exprs)):
+        for i in range(len(off) - 1):
             hdr = int(ops[off[i]])
             ok, reason = reason_for(self.problem_id, int(r['status'][i]), r['res_ref'][i],
                                     float(r['q_ref'][i]), float(r['q_grid'][i]),
@@ -126,13 +129,14 @@ class BatchValidator:
         return out
 
     def validate_strings(self, strings: Sequence[str]) -> List[Verdict]:
-        exprs = []
-        for s in strings:
-            try:
-                exprs.append(self.pd.parse(s))
-            except Exception:   # noqa: BLE001
-                exprs.append(sp.Function('unparsable')(self.pd.x))
-        return self.validate_exprs(exprs)
+        """Candidate strings in: compiled by the native compiler (csrc/pdcompile.cpp), SymPy
+        only for the strings it declines (pdeval/native.py); unparsable strings get the
+        UNSUPPORTED stub and an "Error: ..." reason, as on the SymPy path."""
+        if not strings:
+            return []
+        from .native import compile_strings
+        ops, off, notes = compile_strings(self.pd, list(strings))
+        return self._verdicts(ops, off, notes)
 
     def close(self):
         self.ctx.close()

@@ -156,6 +156,9 @@ def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[s
 
 def process_batch(claimed, validator, kwargs, locs, tagger):
     """(expr_id, expr_str) list -> result tuples of the reference's writer protocol."""
+    if (hasattr(validator, 'validate_strings') and not kwargs.get('check_regularity', False)
+            and not kwargs.get('fast_point_only', False)):
+        return _process_batch_strings(claimed, validator, locs, tagger)
     us, ids, results = [], [], []
     for expr_id, expr_str in claimed:
         try:
@@ -170,6 +173,33 @@ def process_batch(claimed, validator, kwargs, locs, tagger):
             verdicts = [validator.validate(u, **kwargs) for u in us]
         valid = [i for i, (ok, _) in enumerate(verdicts) if ok]
         tags = dict(zip(valid, tagger.tag([us[i] for i in valid])))
+        for i, (ok, reason) in enumerate(verdicts):
+            is_paper, name = tags.get(i, (False, None))
+            results.append(('completed', bool(ok), reason, is_paper, name, ids[i]))
+    return results
+
+
+def _process_batch_strings(claimed, validator, locs, tagger):
+    """Fast path of process_batch: the strings go to the native compiler, SymPy parses only
+    what it cannot (declined strings, parse errors -- whose message the reference reports as
+    'Validator Error: ...', :1703-1714) and the accepted rows (known-solution tagging)."""
+    from .native import COMPILE_PARSE, compile_native
+    pid = validator._validator().problem_id
+    _, _, st = compile_native(pid, [s for _, s in claimed])
+    results, ids, strs = [], [], []
+    for (expr_id, expr_str), t in zip(claimed, st):
+        if t == COMPILE_PARSE:
+            try:
+                sp.sympify(expr_str, locals=locs)
+            except Exception as e:   # noqa: BLE001
+                results.append(('error', None, f'Validator Error: {e}', None, None, expr_id))
+                continue
+        ids.append(expr_id)
+        strs.append(expr_str)
+    if strs:
+        verdicts = validator.validate_strings(strs)
+        valid = [i for i, (ok, _) in enumerate(verdicts) if ok]
+        tags = dict(zip(valid, tagger.tag([sp.sympify(strs[i], locals=locs) for i in valid])))
         for i, (ok, reason) in enumerate(verdicts):
             is_paper, name = tags.get(i, (False, None))
             results.append(('completed', bool(ok), reason, is_paper, name, ids[i]))

@@ -91,6 +91,14 @@ class PreciseFoliationValidator:
                 out[i] = self._memo[key] = r
         return out  # type: ignore[return-value]
 
+    def validate_strings(self, strings: Sequence[str]) -> List[Tuple[bool, str]]:
+        """The driver's queue items are strings (general_method_paper_reproduction.py:1767):
+        validate them without building SymPy trees (native compiler, SymPy only for the
+        strings it declines), with the driver's kwargs check_regularity=False,
+        fast_point_only=False.  Same (bool, reason) as validate_batch(sympify(s))."""
+        res = self._validator().validate_strings(list(strings))
+        return [(v.ok, v.reason) for v in res]
+
     def validate_known_solutions(self) -> Dict[str, bool]:
         rho, z = self.rho, self.z
         known = {

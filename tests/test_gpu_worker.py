@@ -34,3 +34,40 @@ def test_worker_queue_protocol_and_tags():
               'sqrt(rho**2 + z**2) - z', 'rho**2*exp(-2*z)', '-z/sqrt(rho**2 + z**2) + 1',
               'square(rho*exp_neg(z))'):
         assert s in tagged, (s, tagged)
+
+
+def test_worker_string_fast_path_matches_sympy_path():
+    """process_batch on strings (native compiler) == the SymPy-tree path, row for row."""
+    from problems import load_problem
+    from pdeval.worker import KnownSolutionTagger, _process_batch_strings, process_batch
+    rows = G.decided(G.ref_rows(*G.FF_REF, 'ff_edge.jsonl'))
+    claimed = [(i + 1, r['expr']) for i, r in enumerate(rows)] + [(0, 'rho +')]
+    prob = load_problem('force_free')
+    locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
+    tagger = KnownSolutionTagger(prob, locs)
+    kw = {'check_regularity': False, 'fast_point_only': False}
+    fast = sorted(_process_batch_strings(claimed, prob.validator, locs, tagger), key=lambda t: t[5])
+    slow = sorted(_slow(claimed, prob.validator, kw, locs, tagger), key=lambda t: t[5])
+    assert [t[:2] + t[3:] for t in fast] == [t[:2] + t[3:] for t in slow]
+    assert [t[2] for t in fast[1:]] == [t[2] for t in slow[1:]]     # same reason strings
+    assert fast[0][0] == 'error' and fast[0][2].startswith('Validator Error')
+    # process_batch takes the fast path with the driver's kwargs
+    assert sorted(process_batch(claimed, prob.validator, kw, locs, tagger), key=lambda t: t[5]) == fast
+
+
+def _slow(claimed, validator, kw, locs, tagger):
+    import sympy as sp
+    out, us, ids = [], [], []
+    for eid, s in claimed:
+        try:
+            us.append(sp.sympify(s, locals=locs))
+            ids.append(eid)
+        except Exception as e:   # noqa: BLE001
+            out.append(('error', None, str(e), None, None, eid))
+    v = validator.validate_batch(us, **kw)
+    valid = [i for i, (ok, _) in enumerate(v) if ok]
+    tags = dict(zip(valid, tagger.tag([us[i] for i in valid])))
+    for i, (ok, reason) in enumerate(v):
+        t = tags.get(i, (False, None))
+        out.append(('completed', bool(ok), reason, t[0], t[1], ids[i]))
+    return out
