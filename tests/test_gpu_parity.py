@@ -196,3 +196,18 @@ def test_native_compile_full_d4(ff_ctx):
     diff = ok[nat['status'][ok] != ref['status'][ok]]
     assert not diff.size, [(strings[i], int(nat['status'][i]), int(ref['status'][i])) for i in diff[:10]]
     assert np.array_equal(nat['verdict'][ok], ref['verdict'][ok])
+
+
+def test_native_compile_full_kerr_d3(kerr_ctx):
+    """All 16,323 validated Kerr depth<=3 strings: native compile (SymPy for declined ones)
+    vs the SymPy-compiled programs of data/kerr_magnetosphere_d3_validated.npz, same class."""
+    import os
+    from pdeval import native
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             'data', 'kerr_magnetosphere_d3_validated.npz'))
+    strings = [str(s) for s in d['exprs']]
+    ops, off, _ = native.compile_strings(P.kerr(), strings)
+    nat = kerr_ctx.validate(ops, off)
+    ref = kerr_ctx.validate(d['ops'], d['offsets'])
+    diff = np.flatnonzero(nat['status'] != ref['status'])
+    assert not diff.size, [(strings[i], int(nat['status'][i]), int(ref['status'][i])) for i in diff[:10]]
