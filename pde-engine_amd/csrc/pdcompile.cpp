@@ -568,10 +568,7 @@ struct Ctx {
     // ---------------------------------------------------------------- Pow (Pow.__new__)
     static bool half(Rat e) { return e.q == 2; }
     int pow_(int b, int e) {
-        if (!is_num(e)) {
-            if (b == -2) return exp_(e);   // not used: E is declined at parse time
-            throw Decline{};               // symbolic exponents
-        }
+        if (!is_num(e)) throw Decline{};   // symbolic exponents (E**x, rho**z ...)
         const Rat ex = rv(e);
         if (ex.p == 0) return ONE;
         if (req(ex, Rat{1, 1})) return b;
@@ -719,7 +716,6 @@ struct Parser {
     int term() {
         int acc = unary();
         for (;;) {
-            if (peek2("**")) return acc;   // cannot happen here (power binds tighter)
             if (peek('*')) { ++i; acc = C.mul({acc, unary()}); }
             else if (peek('/')) {
                 ++i;
