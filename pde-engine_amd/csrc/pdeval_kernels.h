@@ -868,15 +868,17 @@ void validate_kernel(KernelArgs a) {
             if (active && p < a.n_ref) {
                 if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = r.res_re;
                 if (r.finite && !r.grad_zero) grad_nz = true;
-            } else if (active) {
-                if (r.finite) {
-                    ++nfin;
-                    qmax = fmax(qmax, qv);
-                    if (qv > a.prm.tau_grid) ++nbad;
-                    if (!r.grad_zero) grad_nz = true;
-                } else {
-                    ++nnonfin;
-                }
+            } else if (active && r.finite) {
+                qmax = fmax(qmax, qv);
+                if (!r.grad_zero) grad_nz = true;
+            }
+            // grid counts are wave-uniform (ballot + popcount into SGPRs) rather than per-lane
+            // counters reduced at the end: three fewer live VGPRs across the interpreter loop
+            {
+                const bool g = active && p >= a.n_ref;
+                nfin += (int)__popcll(__ballot(g && r.finite));
+                nbad += (int)__popcll(__ballot(g && r.finite && qv > a.prm.tau_grid));
+                nnonfin += (int)__popcll(__ballot(g && !r.finite));
             }
             if (ch == 0) {
                 // point stage: lanes 0..n_ref-1 hold the reference points
@@ -913,9 +915,6 @@ void validate_kernel(KernelArgs a) {
         }
         // wave reductions
         qmax = wave_max(qmax);
-        nbad = wave_sum(nbad);
-        nnonfin = wave_sum(nnonfin);
-        nfin = wave_sum(nfin);
         const bool any_grad = __any(grad_nz);
         if (lane == 0) {
             int cls = status;

@@ -18,6 +18,8 @@ static pd_dim3 threadIdx, blockIdx, blockDim, gridDim;
 inline double __shfl_xor(double v, int, int) { return v; }
 inline int __shfl_xor(int v, int, int) { return v; }
 inline bool __any(bool v) { return v; }
+inline unsigned long long __ballot(bool v) { return v ? 1ull : 0ull; }
+inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 inline void __builtin_amdgcn_sched_barrier(int) {}
 inline int atomicAdd(int32_t* p, int v) { int o = *p; *p += v; return o; }
