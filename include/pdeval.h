@@ -18,7 +18,10 @@
  *   ops      int32 words of ALL programs, concatenated; program i is ops[offsets[i] ..
  *            offsets[i+1]).  Word = opcode (bits 0-7) | small operand (bits 8-31); opcodes
  *            that carry an f64 immediate are followed by two words holding its IEEE bits
- *            (low word first).
+ *            (low word first); if the immediate is not exactly representable (1/3, 1/10, E)
+ *            the opcode word has PDEVAL_IMM_DD set and two more words follow: the f64 low
+ *            part of the double-double value (value - hi), used by the point stage's
+ *            double-double tier (the fp64 passes skip it).
  *   offsets  int64[n+1], offsets[0] = 0, non-decreasing.
  */
 #ifndef PDEVAL_H
@@ -100,6 +103,10 @@ enum pdeval_opcode {
 
 #define PDEVAL_MAX_STACK  8   /* deepest program stack any kernel variant accepts */
 
+/* Immediate-carrying opcode word (PUSH_C, ADDC, MULC, RDIVC): bit 8 set = a double-double
+   low part follows the f64 immediate (2 more words, low word first).                    */
+#define PDEVAL_IMM_DD     (1u << 8)
+
 /* Program header word: opcode 0 | stack depth << 8 | flags */
 #define PDEVAL_FLAG_COMPLEX  (1u << 16)  /* pushes the imaginary unit: complex pass only   */
 #define PDEVAL_FLAG_NOCOORD  (1u << 17)  /* references no coordinate (u is a constant)   */
@@ -116,12 +123,20 @@ typedef struct pdeval_params {
     int32_t full_grid;   /* 1: evaluate the whole grid for every candidate;
                             0: stop after the point stage for point-rejects (as the
                                reference does, validator.py:371-402)                 */
+    /* (tau_point is kept for ABI compatibility; the point stage is decided by the
+        error-bounded rule of point_abs_tol / res_rel_acc)              */
     int32_t max_bad;     /* grid stage rejects iff n_bad > max_bad                   */
     int32_t strict_symbolic; /* 1: reproduce the reference's symbolic-stage verdict on
                                 non-smooth candidates (PDEVAL_CLS_REJECT_SYMBOLIC)       */
     int32_t reserved;
     double noise_kappa;  /* tier 2: a failing point counts only if |residual| > noise_kappa x
                             its first-order rounding-noise bound     */
+    double point_abs_tol;/* force-free point stage: a residual that is certainly non-zero
+                            rejects if it is rational (an exact Number != 0) or if
+                            |det| >= point_abs_tol = 1e-20 (validator.py:371-397)     */
+    double res_rel_acc;  /* point stage: a residual decided in fp64 must carry a bound
+                            noise_kappa x noise <= res_rel_acc x |res| (1e-11), else it
+                            is re-evaluated in double-double          */
 } pdeval_params;
 
 /* Per-candidate outputs; any pointer may be NULL (not produced).  Host or device memory
@@ -130,7 +145,8 @@ typedef struct pdeval_outputs {
     uint8_t* verdict_bits;   /* ceil(n/8) bytes, bit i = candidate i accepted (LSB first) */
     uint8_t* status;         /* n, PDEVAL_CLS_*                                            */
     double*  q_ref;          /* n, scaled residual at the point stage (Kerr: max |lhs|)    */
-    double*  res_ref;        /* n * n_ref, raw residual at each reference point            */
+    double*  res_ref;        /* n * n_ref, raw residual at each reference point (complex:
+                                its modulus with the sign of its real part)              */
     double*  q_grid;         /* n, max scaled residual over the finite grid points         */
     int32_t* n_bad;          /* n, grid points with q > tau_grid                           */
     int32_t* n_nonfinite;    /* n, grid points where the evaluation was not finite         */
@@ -171,12 +187,14 @@ int pdeval_validate_device(pdeval_ctx* ctx, const int32_t* d_ops, int64_t n_word
  * the launch stream (passes a problem does not run take 0 ms).  pdeval_pass_times waits for
  * the last event of the most recent call and writes min(max_passes, PDEVAL_N_PASSES)
  * durations in ms (and, if names != NULL, a static name per pass).                       */
-#define PDEVAL_N_PASSES 10
+#define PDEVAL_N_PASSES 12
 int pdeval_set_timing(pdeval_ctx* ctx, int enable);
 int pdeval_pass_times(pdeval_ctx* ctx, float* ms, int max_passes, const char** names);
 /* Work-list sizes of the most recent call (synchronizes the device): [0] deferred to the
  * stack-3 pass, [1] complex passes, [2] deferred to the stack-8 pass, [3] tier-2 entries,
- * [4] tier-2 stack 3, [5] tier-2 complex, [6] complex stack 8, [7] tier-2 stack 8.        */
+ * [4] tier-2 stack 3, [5] tier-2 complex, [6] complex stack 8, [7] tier-2 stack 8,
+ * [8] deep point pass (real, stack 3..8), [9] double-double point tier (real),
+ * [10] double-double point tier (complex).                                               */
 int pdeval_pass_counts(pdeval_ctx* ctx, int64_t* counts, int max_counts);
 
 /* Diagnostics (force-free): one program at n_pts points (host arrays), tier-1 (tier2 = 0) or
@@ -185,6 +203,23 @@ int pdeval_pass_counts(pdeval_ctx* ctx, int64_t* counts, int max_counts);
  * coefficients of u then their error bounds.  Synchronous; allocates.  Not a hot path.  */
 int pdeval_eval_points(pdeval_ctx* ctx, const int32_t* prog, int64_t n_words, const double* xs,
                        const double* ys, int n_pts, int tier2, double* out, double* jets);
+
+/* Diagnostics of the point stage (pdeval_point.h).  pdeval_point_eval: one program at the
+ * context's reference points in precision tier 0 (fp64), 1 (complex fp64), 2 (double-double)
+ * or 3 (complex double-double); out[6k..6k+5] = {Re res, Im res, |res|, S, noise bound, finite
+ * (1/0, -1 = program error)} for each reference point k, *state = the tier's point-stage
+ * decision (PDEVAL_PS_* bits).  pdeval_point_states: the point-stage state of every candidate
+ * of the most recent validate call (n bytes; synchronizes).  Not hot paths.                 */
+#define PDEVAL_PS_PASS    1    /* passed the point stage                                   */
+#define PDEVAL_PS_REJECT  2    /* rejected by it (final)                                    */
+#define PDEVAL_PS_COMPLEX 4    /* not real at a reference point: complex passes             */
+#define PDEVAL_PS_PROV    8    /* fp64 pass within the noise: re-decided in double-double if
+                                  the grid rejects                                           */
+#define PDEVAL_PS_GRAD    16   /* non-zero gradient at a reference point                    */
+#define PDEVAL_PS_DD      32   /* undecided in fp64: decided in double-double               */
+int pdeval_point_eval(pdeval_ctx* ctx, const int32_t* prog, int64_t n_words, int tier, double* out,
+                      uint8_t* state);
+int pdeval_point_states(pdeval_ctx* ctx, uint8_t* out, int64_t n);
 
 /* Host-side program analysis (no GPU): required stack depth, or < 0 if malformed.      */
 int pdeval_program_depth(const int32_t* ops, int64_t n_words);

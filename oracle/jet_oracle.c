@@ -18,6 +18,7 @@
  */
 #include <complex.h>
 #include <math.h>
+#include <quadmath.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -89,6 +90,16 @@ static void w_horner(const double* h0, const double* F, double* out, int K) {
     memcpy(out, acc, sizeof(double) * NC(K));
 }
 
+#define CT double
+#define CABS cabs
+#define CREAL creal
+#define CIMAG cimag
+#define CEXP cexp
+#define CLOG clog
+#define RPOW pow
+#define REXP exp
+#define RLOG log
+#define CI I
 #define S double
 #define FN(name) name##_r
 #include "jet_oracle_impl.h"
@@ -96,6 +107,34 @@ static void w_horner(const double* h0, const double* F, double* out, int K) {
 #undef FN
 #define S double complex
 #define FN(name) name##_c
+#include "jet_oracle_impl.h"
+#undef S
+#undef FN
+#undef CT
+#undef CABS
+#undef CREAL
+#undef CIMAG
+#undef CEXP
+#undef CLOG
+#undef RPOW
+#undef REXP
+#undef RLOG
+#undef CI
+/* quad precision (113-bit significand) for the point stage: the reference decides it in exact
+ * arithmetic (validator.py:349-402), so the oracle evaluates the reference points with
+ * coordinates and constants wider than f64 (immediates carry their double-double low part) */
+#define CT __float128
+#define CABS cabsq
+#define CREAL crealq
+#define CIMAG cimagq
+#define CEXP cexpq
+#define CLOG clogq
+#define RPOW powq
+#define REXP expq
+#define RLOG logq
+#define CI ((__complex128)I)
+#define S __complex128
+#define FN(name) name##_q
 #include "jet_oracle_impl.h"
 #undef S
 #undef FN
@@ -168,10 +207,10 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
     double complex cc[NCMAX];
     double W[NCMAX];
     if (cplx) {
-        *rc = run_c(w, nw, x, y, K, 1, cc, tier2 ? W : NULL);
+        *rc = run_c(w, nw, x, y, K, 1, cc, tier2 ? W : NULL, 0.0);
     } else {
         double cr[NCMAX];
-        *rc = run_r(w, nw, x, y, K, 0, cr, tier2 ? W : NULL);
+        *rc = run_r(w, nw, x, y, K, 0, cr, tier2 ? W : NULL, 0.0);
         for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
     }
     if (*rc) return r;
@@ -203,6 +242,70 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
 }
 
 static double scaled(double a, double s) { return s > 0 ? a / s : (a == 0 ? 0 : INFINITY); }
+
+/* ---------------------------------------------------------------- point stage (quad)
+ * The reference points as exact ratios, evaluated in __float128 (constants carry their
+ * double-double low part).  The noise bound is the same first-order E-jet rule as tier 2, in
+ * units of EPSQ (quad unit roundoff 2^-113, with a 32x margin for libquadmath's transcendentals). */
+#define EPSQ 0x1p-108
+static void ref_point_q(int problem, int k, __float128* x, __float128* y) {
+    static const int ff[1][4] = {{4, 5, 6, 7}};
+    static const int kr[3][4] = {{5, 2, 3, 5}, {7, 3, 1, 3}, {5, 1, -2, 5}};
+    const int* t = problem == PDEVAL_PROBLEM_FORCE_FREE ? ff[k] : kr[k];
+    *x = (__float128)t[0] / t[1];
+    *y = (__float128)t[2] / t[3];
+}
+
+static __complex128 kerr_lhs_q(__float128 r, __float128 x, const __complex128* c, double* scale) {
+    const __float128 M = 1, a = (__float128)1 / 10;
+    __float128 s = r * r + a * a * x * x;
+    __float128 G = 1 - 2 * M * r / s;
+    __float128 Gr = -2 * M / s + 4 * M * r * r / (s * s);
+    __float128 Gx = 4 * M * r * a * a * x / (s * s);
+    __float128 D = r * r - 2 * M * r + a * a, w = 1 - x * x;
+    __complex128 t[4] = {G / w * 2 * c[IDX(2, 0)], Gr / w * c[IDX(1, 0)], G / D * 2 * c[IDX(0, 2)],
+                         Gx / D * c[IDX(0, 1)]};
+    *scale = (double)(cabsq(t[0]) + cabsq(t[1]) + cabsq(t[2]) + cabsq(t[3]));
+    return t[0] + t[1] + t[2] + t[3];
+}
+
+/* value, scale and noise bound of one program at reference point k, in quad precision */
+static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, int cplx, int* rc) {
+    pt_result r = {0};
+    const int K = problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    __float128 x, y;
+    ref_point_q(problem, k, &x, &y);
+    __complex128 cq[NCMAX];
+    double W[NCMAX];
+    /* the reference points are quad-rounded: 2^-113 relative, 1/32 of EPSQ */
+    *rc = run_q(w, nw, x, y, K, cplx, cq, W, 1.0 / 32);
+    if (*rc) return r;
+    int fin = 1;
+    double complex cd[NCMAX], cp[NCMAX];
+    for (int i = 0; i < NC(K); ++i) {
+        fin = fin && fabsq(crealq(cq[i])) < 0x1p160Q && fabsq(cimagq(cq[i])) < 0x1p160Q;
+        cd[i] = (double)cabsq(cq[i]);
+        cp[i] = cd[i] + NOISE_GAMMA * W[i];
+    }
+    __complex128 res;
+    double S2;
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+        res = ff_det_q(cq, x, 0);
+        r.scale = creal(ff_det_c(cd, (double)x, 1));
+        S2 = creal(ff_det_c(cp, (double)x, 1));
+    } else {
+        double complex dummy;
+        res = kerr_lhs_q(x, y, cq, &r.scale);
+        kerr_terms((double)x, (double)y, cp, 0, &dummy, &S2);
+    }
+    r.noise = (S2 - r.scale) * (EPSQ / NOISE_GAMMA) + EPSQ * r.scale;
+    r.res_abs = (double)cabsq(res);
+    r.res_re = (double)crealq(res);
+    r.finite = fin && finiteq(crealq(res)) && finiteq(cimagq(res)) && isfinite(r.scale) && isfinite(r.noise);
+    r.grad_zero = cq[IDX(1, 0)] == 0 && cq[IDX(0, 1)] == 0;
+    r.u0 = (double)crealq(cq[0]);
+    return r;
+}
 
 /* Validate n programs; outputs as in pdeval_outputs (host arrays, any may be NULL).
  * Returns 0.  Candidate classes follow include/pdeval.h. */
@@ -239,35 +342,30 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
             for (int f = 0; f < PDEVAL_FP_N; ++f)
                 if (p == fp[f] && fingerprint) fingerprint[ci * PDEVAL_FP_N + f] = r.u0;
             if (p < nref) {
-                if (res_ref) res_ref[ci * nref + p] = r.res_re;
                 if (r.finite && !r.grad_zero) any_grad = 1;
-                double v = problem == PDEVAL_PROBLEM_FORCE_FREE ? scaled(r.res_abs, r.scale) : r.res_abs;
-                if (!r.finite) {
+                /* the point stage, in quad precision (validator.py:349-402 / kerr :163-192):
+                 * force-free rejects a residual that is certainly non-zero (beyond kappa x
+                 * its noise bound) when it is rational (an exact Number != 0) or >= 1e-20;
+                 * Kerr rejects max |lhs| >= 1e-10 */
+                int rcq;
+                pt_result q = eval_point_q(problem, w, nw, p, cplx, &rcq);
+                if (rcq == -2 || rcq == -3) { cls = PDEVAL_CLS_UNSUPPORTED; break; }
+                if (rcq) { cls = PDEVAL_CLS_BAD_PROGRAM; break; }
+                /* a complex residual is reported as its modulus with the sign of its real part */
+                if (res_ref) res_ref[ci * nref + p] = copysign(q.res_abs, q.res_re);
+                if (!q.finite) {
                     if (problem == PDEVAL_PROBLEM_FORCE_FREE && !cplx) { cplx = 1; goto again; }
-                    point_reject = 2;    /* non-finite at a reference point: final */
-                } else if (!(qr >= v)) {
-                    qr = v;
+                    point_reject = 1;    /* non-finite at a reference point: final */
+                } else if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+                    qr = scaled(q.res_abs, q.scale);
+                    if (q.res_abs > prm->noise_kappa * q.noise &&
+                        ((hdr & PDEVAL_FLAG_RATIONAL) || q.res_abs >= prm->point_abs_tol))
+                        point_reject = 1;
+                } else {
+                    if (!(qr >= q.res_abs)) qr = q.res_abs;
+                    if (q.res_abs >= prm->kerr_abs_tol) point_reject = 1;
                 }
-                if (p == nref - 1) {
-                    if (!point_reject) {
-                        if (problem == PDEVAL_PROBLEM_FORCE_FREE) point_reject = !(qr <= prm->tau_point);
-                        else point_reject = !(qr < prm->kerr_abs_tol);
-                    }
-                    if (point_reject == 1) {
-                        /* tier 2: a point-stage failure stands only where the residual also
-                         * exceeds its rounding-noise bound */
-                        point_reject = 0;
-                        for (int p2 = 0; p2 < nref; ++p2) {
-                            int rc2;
-                            pt_result r2 = eval_point(problem, w, nw, px[p2], py[p2], cplx, 1, &rc2);
-                            double v2 = problem == PDEVAL_PROBLEM_FORCE_FREE ? scaled(r2.res_abs, r2.scale) : r2.res_abs;
-                            int fails = problem == PDEVAL_PROBLEM_FORCE_FREE ? !(v2 <= prm->tau_point)
-                                                                             : !(v2 < prm->kerr_abs_tol);
-                            if (fails && r2.res_abs > prm->noise_kappa * r2.noise) point_reject = 1;
-                        }
-                    }
-                    if (point_reject && !prm->full_grid) cls = PDEVAL_CLS_REJECT_POINT;
-                }
+                if (p == nref - 1 && point_reject && !prm->full_grid) cls = PDEVAL_CLS_REJECT_POINT;
                 continue;
             }
             if (r.finite) {
@@ -318,10 +416,10 @@ int oracle_jet(int problem, const int32_t* w, int64_t nw, double x, double y, in
     double complex cc[NCMAX];
     int rc;
     if (cplx) {
-        rc = run_c(w, nw, x, y, K, 1, cc, NULL);
+        rc = run_c(w, nw, x, y, K, 1, cc, NULL, 0.0);
     } else {
         double cr[NCMAX];
-        rc = run_r(w, nw, x, y, K, 0, cr, NULL);
+        rc = run_r(w, nw, x, y, K, 0, cr, NULL, 0.0);
         for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
     }
     for (int i = 0; i < NC(K) && !rc; ++i) { re[i] = creal(cc[i]); im[i] = cimag(cc[i]); }

@@ -1,6 +1,10 @@
-/* jet_oracle_impl.h -- scalar-type-generic part of the CPU oracle (included twice by
- * jet_oracle.c: once with S = double for the real pass, once with S = double complex for the
- * complex pass).  TEST INFRASTRUCTURE ONLY: never linked into libpdeval.
+/* jet_oracle_impl.h -- scalar-type-generic part of the CPU oracle (included three times by
+ * jet_oracle.c: S = double for the real pass, S = double complex for the complex pass, and
+ * S = __complex128 with quad-precision coordinates and constants (CT = __float128) for the
+ * point stage, which the reference decides in exact arithmetic).  TEST INFRASTRUCTURE ONLY:
+ * never linked into libpdeval.
+ * Per instantiation the includer defines S, CT (coordinate / constant type), FN(name) and the
+ * math macros CABS CREAL CIMAG CEXP CLOG RPOW REXP RLOG RFLOOR CI (the imaginary unit).
  *
  * Derivatives are taken by truncated bivariate Taylor arithmetic (the same mathematics as
  * sp.diff in problems/force_free/validator.py:305-344, evaluated at a point instead of
@@ -62,36 +66,44 @@ static void FN(jcompose)(S* x, const S* f, int K) {
 /* principal-branch x0**alpha, with the real pass undefined off the real domain */
 static S FN(spow)(S x, double a, int cplx_pass) {
     if (!cplx_pass) {
-        double xr = creal(x);
-        if (a == floor(a)) return pow(xr, a);
+        CT xr = CREAL(x);
+        if (a == floor(a)) return RPOW(xr, (CT)a);
         if (xr < 0) return NAN;
-        return pow(xr, a);
+        return RPOW(xr, (CT)a);
     }
     if (x == 0) return a > 0 ? 0 : INFINITY;
-    return cexp(a * clog(x));
+    return CEXP((CT)a * CLOG(x));
 }
 
-static void FN(wabs)(const S* v, double* w, int K) { for (int i = 0; i < NC(K); ++i) w[i] = cabs(v[i]); }
+static void FN(wabs)(const S* v, double* w, int K) { for (int i = 0; i < NC(K); ++i) w[i] = (double)CABS(v[i]); }
 
 /* Evaluate a program at (px, py).  eout != NULL: also carry the first-order rounding-error
  * jet E (rules at w_mul in jet_oracle.c) and return it. */
-static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, int cplx_pass, S* out,
-                   double* eout) {
+/* cerr: relative rounding of the coordinates in noise units (0 on the exact grid points) */
+static int FN(run)(const int32_t* w, int64_t nw, CT px, CT py, int K, int cplx_pass, S* out,
+                   double* eout, double cerr) {
     S st[16][NCMAX];
     double es[16][NCMAX];
     const int trk = eout != NULL;
     int d = 0;
     for (int64_t pc = 1; pc < nw;) {
         uint32_t word = (uint32_t)w[pc], op = word & 0xffu;
-        double imm = 0;
+        CT imm = 0;
         if (op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC || op == PDOP_POW) {
-            if (pc + 2 >= nw + 1) return -1;
-            uint64_t bits = (uint64_t)(uint32_t)w[pc + 1] | ((uint64_t)(uint32_t)w[pc + 2] << 32);
-            memcpy(&imm, &bits, 8);
-            pc += 3;
+            const int nimm = (word & PDEVAL_IMM_DD) ? 2 : 1;
+            if (pc + 2 * nimm >= nw + 1) return -1;
+            for (int k = 0; k < nimm; ++k) {
+                double v;
+                uint64_t bits = (uint64_t)(uint32_t)w[pc + 1 + 2 * k] | ((uint64_t)(uint32_t)w[pc + 2 + 2 * k] << 32);
+                memcpy(&v, &bits, 8);
+                /* the double-double low part matters only where constants are wider than f64 */
+                if (k == 0 || sizeof(CT) > sizeof(double)) imm += (CT)v;
+            }
+            pc += 1 + 2 * nimm;
         } else {
             pc += 1;
         }
+        const double immd = (double)imm;
         S* t = d > 0 ? st[d - 1] : NULL;
         S* u = d > 1 ? st[d - 2] : NULL;
         double* et = d > 0 ? es[d - 1] : NULL;
@@ -103,17 +115,19 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
                 if (op == PDOP_PUSH_X) { FN(jconst)(st[d], px); st[d][IDX(1, 0)] = 1; }
                 else if (op == PDOP_PUSH_Y) { FN(jconst)(st[d], py); st[d][IDX(0, 1)] = 1; }
                 else if (op == PDOP_PUSH_C) FN(jconst)(st[d], imm);
-                else { if (!cplx_pass) return -2; FN(jconst)(st[d], I); }
+                else { if (!cplx_pass) return -2; FN(jconst)(st[d], CI); }
                 if (trk) {
                     for (int i = 0; i < NCMAX; ++i) es[d][i] = 0;
-                    if (op == PDOP_PUSH_C) es[d][0] = fabs(imm);
+                    if (op == PDOP_PUSH_C) es[d][0] = fabs(immd);
+                    else if (op == PDOP_PUSH_X) es[d][0] = fabs((double)px) * cerr;
+                    else if (op == PDOP_PUSH_Y) es[d][0] = fabs((double)py) * cerr;
                 }
                 ++d;
                 break;
             case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB:
                 for (int i = 0; i < NC(K); ++i)
                     u[i] = op == PDOP_ADD ? u[i] + t[i] : (op == PDOP_SUB ? u[i] - t[i] : t[i] - u[i]);
-                if (trk) for (int i = 0; i < NC(K); ++i) eu[i] += et[i] + cabs(u[i]);
+                if (trk) for (int i = 0; i < NC(K); ++i) eu[i] += et[i] + (double)CABS(u[i]);
                 --d;
                 break;
             case PDOP_MUL:
@@ -140,10 +154,10 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
                 --d;
                 break;
             }
-            case PDOP_ADDC: t[0] += imm; if (trk) et[0] += fabs(imm) + cabs(t[0]); break;
+            case PDOP_ADDC: t[0] += imm; if (trk) et[0] += fabs(immd) + (double)CABS(t[0]); break;
             case PDOP_MULC:
                 for (int i = 0; i < NC(K); ++i) t[i] *= imm;
-                if (trk) for (int i = 0; i < NC(K); ++i) et[i] = et[i] * fabs(imm) + cabs(t[i]);
+                if (trk) for (int i = 0; i < NC(K); ++i) et[i] = et[i] * fabs(immd) + (double)CABS(t[i]);
                 break;
             case PDOP_RDIVC: {
                 S c[NCMAX];
@@ -153,7 +167,7 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
                 if (trk) {
                     FN(wabs)(t, R, K);
                     w_mul(R, T2, A, K);
-                    A[0] += fabs(imm);
+                    A[0] += fabs(immd);
                     w_absdiv(A, B, et, K);
                     for (int i = 0; i < NC(K); ++i) et[i] += R[i];
                 }
@@ -170,14 +184,14 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
                 v[ax ? IDX(0, 1) : IDX(1, 0)] = 1;
                 memcpy(pj, v, sizeof pj);
                 for (int k = 1; k < n; ++k) FN(jmul)(pj, v, pj, K);
-                if (trk) { FN(wabs)(pj, P_, K); for (int i = 0; i < NC(K); ++i) ep[i] = n * P_[i]; }
+                if (trk) { FN(wabs)(pj, P_, K); for (int i = 0; i < NC(K); ++i) ep[i] = n * P_[i] * (1 + cerr); }
                 if (op == PDOP_PUSH_P) {
                     memcpy(st[d], pj, sizeof(S) * NCMAX);
                     if (trk) memcpy(es[d], ep, sizeof(double) * NCMAX);
                     ++d;
                 } else if (op == PDOP_ADD_P || op == PDOP_SUB_P) {
                     for (int i = 0; i < NC(K); ++i) t[i] = op == PDOP_ADD_P ? t[i] + pj[i] : t[i] - pj[i];
-                    if (trk) for (int i = 0; i < NC(K); ++i) et[i] += ep[i] + cabs(t[i]);
+                    if (trk) for (int i = 0; i < NC(K); ++i) et[i] += ep[i] + (double)CABS(t[i]);
                 } else if (op == PDOP_MUL_P) {
                     if (trk) {
                         FN(wabs)(t, A, K);
@@ -206,10 +220,10 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
                 break;
             }
             case PDOP_NEG: for (int i = 0; i < NC(K); ++i) t[i] = -t[i]; break;
-            case PDOP_ADD_X: t[0] += px; t[IDX(1, 0)] += 1; if (trk) et[0] += cabs(t[0]); break;
-            case PDOP_ADD_Y: t[0] += py; t[IDX(0, 1)] += 1; if (trk) et[0] += cabs(t[0]); break;
-            case PDOP_SUB_X: t[0] -= px; t[IDX(1, 0)] -= 1; if (trk) et[0] += cabs(t[0]); break;
-            case PDOP_SUB_Y: t[0] -= py; t[IDX(0, 1)] -= 1; if (trk) et[0] += cabs(t[0]); break;
+            case PDOP_ADD_X: t[0] += px; t[IDX(1, 0)] += 1; if (trk) et[0] += (double)CABS(t[0]) + fabs((double)px) * cerr; break;
+            case PDOP_ADD_Y: t[0] += py; t[IDX(0, 1)] += 1; if (trk) et[0] += (double)CABS(t[0]) + fabs((double)py) * cerr; break;
+            case PDOP_SUB_X: t[0] -= px; t[IDX(1, 0)] -= 1; if (trk) et[0] += (double)CABS(t[0]) + fabs((double)px) * cerr; break;
+            case PDOP_SUB_Y: t[0] -= py; t[IDX(0, 1)] -= 1; if (trk) et[0] += (double)CABS(t[0]) + fabs((double)py) * cerr; break;
             case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: {
                 S v[NCMAX];
                 int isx = (op == PDOP_MUL_X || op == PDOP_DIV_X);
@@ -217,11 +231,16 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
                 v[isx ? IDX(1, 0) : IDX(0, 1)] = 1;
                 if (trk) { FN(wabs)(v, B, K); memcpy(T1, et, sizeof T1); }
                 if (op == PDOP_MUL_X || op == PDOP_MUL_Y) {
+                    double cv[NCMAX];
+                    if (trk) { FN(wabs)(t, cv, K); for (int i = 0; i < NC(K); ++i) cv[i] *= B[0] * cerr; }
                     FN(jmul)(t, v, t, K);
-                    if (trk) { w_mul(T1, B, et, K); FN(wabs)(t, R, K); for (int i = 0; i < NC(K); ++i) et[i] += R[i]; }
+                    if (trk) { w_mul(T1, B, et, K); FN(wabs)(t, R, K); for (int i = 0; i < NC(K); ++i) et[i] += R[i] + cv[i]; }
                 } else {
                     FN(jdiv)(t, v, t, K);
-                    if (trk) { FN(wabs)(t, R, K); w_absdiv(T1, B, et, K); for (int i = 0; i < NC(K); ++i) et[i] += R[i]; }
+                    if (trk) {
+                        FN(wabs)(t, R, K); w_absdiv(T1, B, et, K);
+                        for (int i = 0; i < NC(K); ++i) et[i] += R[i] + R[i] * cerr * (K + 1);
+                    }
                 }
                 break;
             }
@@ -244,20 +263,20 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
             case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: {
                 S x0 = t[0];
                 if (op == PDOP_POW || op == PDOP_SQRT) {
-                    double a = (op == PDOP_SQRT) ? 0.5 : imm;
+                    double a = (op == PDOP_SQRT) ? 0.5 : immd;
                     f[0] = FN(spow)(x0, a, cplx_pass);
-                    for (int k = 1; k <= K + 1; ++k) f[k] = f[k - 1] * ((a - (k - 1)) / k) / x0;
+                    for (int k = 1; k <= K + 1; ++k) f[k] = f[k - 1] * ((CT)(a - (k - 1)) / k) / x0;
                 } else if (op == PDOP_EXP) {
-                    S e = cplx_pass ? cexp(x0) : exp(creal(x0));
-                    double fact = 1;
+                    S e = cplx_pass ? CEXP(x0) : REXP(CREAL(x0));
+                    CT fact = 1;
                     for (int k = 0; k <= K + 1; ++k) { if (k) fact *= k; f[k] = e / fact; }
                 } else {
-                    f[0] = cplx_pass ? clog(x0) : (creal(x0) > 0 ? log(creal(x0)) : (creal(x0) == 0 ? -INFINITY : NAN));
-                    for (int k = 1; k <= K + 1; ++k) f[k] = ((k & 1) ? 1.0 : -1.0) / (k * FN(spow)(x0, k, cplx_pass));
+                    f[0] = cplx_pass ? CLOG(x0) : (CREAL(x0) > 0 ? RLOG(CREAL(x0)) : (CREAL(x0) == 0 ? -INFINITY : NAN));
+                    for (int k = 1; k <= K + 1; ++k) f[k] = (CT)((k & 1) ? 1.0 : -1.0) / (k * FN(spow)(x0, k, cplx_pass));
                 }
                 if (trk) {
                     double G[KMAX + 1], Fa[KMAX + 1];
-                    for (int k = 0; k <= K; ++k) { G[k] = (k + 1) * cabs(f[k + 1]); Fa[k] = cabs(f[k]); }
+                    for (int k = 0; k <= K; ++k) { G[k] = (k + 1) * (double)CABS(f[k + 1]); Fa[k] = (double)CABS(f[k]); }
                     FN(wabs)(t, A, K);
                     w_horner(A, G, T1, K);         /* G1 = sum (m+1)|f_(m+1)| |h|^m */
                     w_horner(A, Fa, R, K);         /* sum |f_k| |h|^k */
@@ -269,8 +288,8 @@ static int FN(run)(const int32_t* w, int64_t nw, double px, double py, int K, in
             }
             case PDOP_ABS: {
                 double sg;
-                if (cimag(t[0]) != 0) sg = NAN;
-                else sg = creal(t[0]) > 0 ? 1 : (creal(t[0]) < 0 ? -1 : NAN);
+                if (CIMAG(t[0]) != 0) sg = NAN;
+                else sg = CREAL(t[0]) > 0 ? 1 : (CREAL(t[0]) < 0 ? -1 : NAN);
                 for (int i = 0; i < NC(K); ++i) t[i] *= sg;
                 break;
             }
@@ -293,8 +312,8 @@ static S FN(partial)(const S* c, int i, int j) {
 
 /* Force-free determinant in closed form from partials (validator.py:323-347, Omega = 0).
  * mag != 0: every term replaced by its magnitude (the scale S). */
-static S FN(ff_det)(const S* c, double rho, int mag) {
-#define M_(x) (mag ? (S)cabs(x) : (x))
+static S FN(ff_det)(const S* c, CT rho, int mag) {
+#define M_(x) (mag ? (S)CABS(x) : (x))
 #define SUB_(a, b) (mag ? ((a) + (b)) : ((a) - (b)))
     S u10 = M_(FN(partial)(c, 1, 0)), u01 = M_(FN(partial)(c, 0, 1));
     S u20 = M_(FN(partial)(c, 2, 0)), u11 = M_(FN(partial)(c, 1, 1)), u02 = M_(FN(partial)(c, 0, 2));
@@ -302,7 +321,7 @@ static S FN(ff_det)(const S* c, double rho, int mag) {
     S u03 = M_(FN(partial)(c, 0, 3));
     S u40 = M_(FN(partial)(c, 4, 0)), u31 = M_(FN(partial)(c, 3, 1)), u22 = M_(FN(partial)(c, 2, 2));
     S u13 = M_(FN(partial)(c, 1, 3)), u04 = M_(FN(partial)(c, 0, 4));
-    double r1 = 1.0 / rho, r2 = r1 * r1, r3 = r2 * r1;
+    CT r1 = 1 / rho, r2 = r1 * r1, r3 = r2 * r1;
     S p = u10, q = u01;
     /* A = u20 + u02 - u10/rho and its partials */
     S Ar = u30 + u12 + SUB_(0, u20 * r1) + u10 * r2;

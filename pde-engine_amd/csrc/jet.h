@@ -19,6 +19,8 @@
 
 #define PD_HD __host__ __device__ __forceinline__
 
+#include "dd.h"
+
 namespace pd {
 
 PD_HD constexpr int nc(int K) { return (K + 1) * (K + 2) / 2; }
@@ -36,12 +38,34 @@ PD_HD cplx operator*(cplx a, cplx b) {
 }
 PD_HD cplx operator*(cplx a, double s) { return {a.re * s, a.im * s}; }
 
-template <class T> PD_HD T zero();
 template <> PD_HD double zero<double>() { return 0.0; }
 template <> PD_HD cplx zero<cplx>() { return {0.0, 0.0}; }
-template <class T> PD_HD T from_real(double v);
 template <> PD_HD double from_real<double>(double v) { return v; }
 template <> PD_HD cplx from_real<cplx>(double v) { return {v, 0.0}; }
+
+// Coordinates and constants enter the jets as V = double (fp64 and complex passes) or V = dd
+// (the double-double point tier, dd.h); cvt<T>(v) converts them to the jet scalar T.
+template <class T, class V> struct Cvt {
+    static PD_HD T f(double v) { return from_real<T>(v); }
+};
+template <> struct Cvt<dd, dd> { static PD_HD dd f(dd v) { return v; } };
+template <> struct Cvt<cdd, dd> { static PD_HD cdd f(dd v) { return {v, {0.0, 0.0}}; } };
+template <class T, class V> PD_HD T cvt(V v) { return Cvt<T, V>::f(v); }
+PD_HD double rcp(double v) { return 1.0 / v; }
+PD_HD dd rcp(dd v) { return recip(v); }
+PD_HD double vabs(double v) { return fabs(v); }
+PD_HD double vabs(dd v) { return fabs(v.hi); }
+// v * num / k for a Taylor-coefficient recurrence: fp64 scales by the rounded num / k (as
+// the fp64 passes always have); the double-double tier divides exactly-rounded (1/3 is not
+// a double)
+PD_HD double divk(double v, double num, int k) { return v * (num / k); }
+PD_HD cplx divk(cplx v, double num, int k) { return v * (num / k); }
+PD_HD dd divk(dd v, double num, int k) { return dd_div(v * num, (double)k); }
+PD_HD cdd divk(cdd v, double num, int k) { return {dd_div(v.re * num, (double)k), dd_div(v.im * num, (double)k)}; }
+template <class V> PD_HD V vone() { return V(1.0); }
+template <> PD_HD dd vone<dd>() { return {1.0, 0.0}; }
+template <class V> PD_HD V vzero() { return V(0.0); }
+template <> PD_HD dd vzero<dd>() { return {0.0, 0.0}; }
 
 PD_HD double fmac(double a, double b, double c) { return fma(a, b, c); }
 PD_HD cplx fmac(cplx a, cplx b, cplx c) {
@@ -225,7 +249,7 @@ template <class T, int K> PD_HD void coef_pow(T x0, double alpha, T f0, T* f) {
     const T r = recip(x0);
     f[0] = f0;
 #pragma unroll
-    for (int k = 1; k <= K; ++k) f[k] = f[k - 1] * r * ((alpha - (k - 1)) / k);
+    for (int k = 1; k <= K; ++k) f[k] = divk(f[k - 1] * r, alpha - (k - 1), k);
 }
 
 }  // namespace pd

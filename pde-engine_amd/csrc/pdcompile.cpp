@@ -799,7 +799,9 @@ enum IK : uint8_t { IX, IY, IC, INEG, ISQRT, IEXP, IABS, IPOWN, IPOW, IADD, ISUB
 struct IR {
     IK k;
     double c = 0.0;   // IC value / IPOW exponent
-    bool irr = false; // IC: irrational constant (E), flatten.py's ('c', v, False)
+    double lo = 0.0;  // IC: low part of the double-double value (PDEVAL_IMM_DD), 0 if c is exact
+    Rat r{0, 1};      // IC: exact value (rational constants)
+    bool irr = false; // IC: irrational constant (E), flatten.py's ('c', v, e, False)
     Rat alpha;        // IPOW exact exponent (det_rational)
     int n = 0;        // IPOWN
     int a = -1, b = -1;
@@ -810,8 +812,17 @@ struct Lower {
     std::vector<IR> ir;
     explicit Lower(Ctx& c) : C(c) {}
     int mk(IR x) { ir.push_back(x); return (int)ir.size() - 1; }
-    int cst(double v) { IR x{IC}; x.c = v; return mk(x); }
     static double rdouble(Rat r) { return (double)r.p / (double)r.q; }   // exact p, q: correctly rounded
+    // low part of p/q - rdouble(p/q): hi*q = P + e exactly (FMA), P - p is exact (Sterbenz)
+    static double rlo(Rat r, double hi) {
+        const double q = (double)r.q;
+        const double P = hi * q, e = std::fma(hi, q, -P);
+        return -((P - (double)r.p) + e) / q;
+    }
+    int cst(Rat r) { IR x{IC}; x.r = r; x.c = rdouble(r); x.lo = rlo(r, x.c); return mk(x); }
+    // E = exp(1) and 1/E as double-doubles (flatten.py E_EXACT)
+    static constexpr double kE = 0x1.5bf0a8b145769p+1, kELo = 0x1.4d57ee2b1013ap-53;
+    static constexpr double kInvE = 0x1.78b56362cef38p-2, kInvELo = -0x1.ca8a4270fadf5p-57;
     int un(IK k, int a) { IR x{k}; x.a = a; return mk(x); }
     int bin(IK k, int a, int b) { IR x{k}; x.a = a; x.b = b; return mk(x); }
     bool is_pvar(int i) const {
@@ -846,14 +857,14 @@ struct Lower {
                 const SymInfo& si = C.syms[nd.sym];
                 if (si.coord == 0) return mk(IR{IX});
                 if (si.coord == 1) return mk(IR{IY});
-                return cst(rdouble(si.value));
+                return cst(si.value);
             }
-            case NUM: return cst(rdouble(nd.r));
+            case NUM: return cst(nd.r);
             case ADD: return add(e);
             case MUL: return mulnode(e);
             case POW: return pownode(nd.a[0], nd.a[1]);
             case EXP:
-                if (nd.a[0] == C.ONE) { IR x{IC}; x.c = 2.718281828459045; x.irr = true; return mk(x); }
+                if (nd.a[0] == C.ONE) { IR x{IC}; x.c = kE; x.lo = kELo; x.irr = true; return mk(x); }
                 return un(IEXP, node(nd.a[0]));
             case ABS: return un(IABS, node(nd.a[0]));
         }
@@ -865,11 +876,11 @@ struct Lower {
     }
     int add(int e) {
         const Node& nd = C.N(e);
-        double cs = 0.0;
+        Rat cs{0, 1};
         bool have = false;
         std::vector<std::pair<int, int>> terms;   // (sign, ir)
         for (int t : nd.a) {
-            if (C.is_num(t)) { cs += rdouble(C.rv(t)); have = true; continue; }
+            if (C.is_num(t)) { cs = radd(cs, C.rv(t)); have = true; continue; }
             int sg = 1;
             int tt = t;
             if (C.N(t).k == MUL) {
@@ -893,7 +904,7 @@ struct Lower {
         if (terms[0].first < 0) acc = un(INEG, acc);
         for (size_t k = 1; k < terms.size(); ++k)
             acc = bin(terms[k].first > 0 ? IADD : ISUB, acc, terms[k].second);
-        if (have && cs != 0.0) acc = bin(IADD, acc, cst(cs));
+        if (have && cs.p != 0) acc = bin(IADD, acc, cst(cs));
         return acc;
     }
     int mulnode(int e) { return mulargs(e, Rat{1, 1}); }
@@ -902,10 +913,10 @@ struct Lower {
         std::vector<int> fs;
         if (C.N(e).k == MUL) fs = C.N(e).a;
         else if (e != C.ONE) fs.push_back(e);
-        double coef = 1.0;
+        Rat coef{1, 1};
         bool first = true;
         auto mulc = [&](Rat r) {
-            coef *= rdouble(r);
+            coef = rmul(coef, r);
             first = false;
         };
         if (!req(extra, Rat{1, 1})) mulc(extra);
@@ -932,8 +943,8 @@ struct Lower {
         if (!num.empty()) {
             int acc = product(num);
             if (!den.empty()) acc = bin(IDIV, acc, product(den));
-            if (coef == -1.0) acc = un(INEG, acc);
-            else if (coef != 1.0) acc = bin(IMUL, acc, cst(coef));
+            if (req(coef, Rat{-1, 1})) acc = un(INEG, acc);
+            else if (!req(coef, Rat{1, 1})) acc = bin(IMUL, acc, cst(coef));
             return acc;
         }
         if (!den.empty()) return bin(IDIV, cst(coef), product(den));
@@ -943,10 +954,10 @@ struct Lower {
         if (!C.is_num(ex)) throw Decline{};
         const Rat e = C.rv(ex);
         if (rint(e)) {
-            if (e.p == 0) return cst(1.0);
+            if (e.p == 0) return cst(Rat{1, 1});
             const int b = node(base);
             if (e.p > 0) return pown(b, (int)std::min<int64_t>(e.p, 1 << 20));
-            return bin(IDIV, cst(1.0), pown(b, (int)std::min<int64_t>(-e.p, 1 << 20)));
+            return bin(IDIV, cst(Rat{1, 1}), pown(b, (int)std::min<int64_t>(-e.p, 1 << 20)));
         }
         const int b = node(base);
         if (req(e, Rat{1, 2})) return un(ISQRT, b);
@@ -1042,12 +1053,17 @@ struct Emit {
             --d;
         }
     }
-    void opi(int code, double imm) {
-        op(code);
+    void word64(double v) {
         uint64_t u;
-        memcpy(&u, &imm, 8);
+        memcpy(&u, &v, 8);
         w.push_back((int32_t)(uint32_t)(u & 0xffffffffu));
         w.push_back((int32_t)(uint32_t)(u >> 32));
+    }
+    // immediate hi (+ double-double low part lo, flagged PDEVAL_IMM_DD, when it is not 0)
+    void opi(int code, double imm, double lo = 0.0) {
+        op(code, lo != 0.0 ? (int)(PDEVAL_IMM_DD >> 8) : 0);
+        word64(imm);
+        if (lo != 0.0) word64(lo);
     }
     int parg(int i) const { return L.ir[i].n | ((L.ir[L.ir[i].a].k == IX ? 0 : 1) << 8); }
     void leaf(int i) {
@@ -1055,7 +1071,7 @@ struct Emit {
         if (L.is_pvar(i)) op(PDOP_PUSH_P, parg(i));
         else if (x.k == IX) op(PDOP_PUSH_X);
         else if (x.k == IY) op(PDOP_PUSH_Y);
-        else opi(PDOP_PUSH_C, x.c);
+        else opi(PDOP_PUSH_C, x.c, x.lo);
     }
     void fused(IK k, int lf) {
         const IR& x = L.ir[lf];
@@ -1065,10 +1081,16 @@ struct Emit {
         }
         if (x.k == IC) {
             const double c = x.c;
-            if (k == IADD) opi(PDOP_ADDC, c);
-            else if (k == ISUB) opi(PDOP_ADDC, -c);
-            else if (k == IMUL) { if (c == -1.0) op(PDOP_NEG); else opi(PDOP_MULC, c); }
-            else opi(PDOP_MULC, 1.0 / c);
+            if (k == IADD) opi(PDOP_ADDC, c, x.lo);
+            else if (k == ISUB) opi(PDOP_ADDC, -c, -x.lo);
+            else if (k == IMUL) { if (c == -1.0) op(PDOP_NEG); else opi(PDOP_MULC, c, x.lo); }
+            else if (x.irr) opi(PDOP_MULC, Lower::kInvE, Lower::kInvELo);     // / E (flatten.py _crecip)
+            else if (x.r.p == 0) opi(PDOP_MULC, 1.0 / c);
+            else {
+                const Rat inv = x.r.p < 0 ? Rat{-x.r.q, -x.r.p} : Rat{x.r.q, x.r.p};
+                const double hi = Lower::rdouble(inv);
+                opi(PDOP_MULC, hi, Lower::rlo(inv, hi));
+            }
             return;
         }
         const bool isx = x.k == IX;
@@ -1094,7 +1116,7 @@ struct Emit {
         if (L.is_leaf(b)) { emit(a); fused(k, b); return; }
         if (L.is_leaf(a) && (k == IADD || k == IMUL)) { emit(b); fused(k, a); return; }
         if (L.is_leaf(a) && k == ISUB) { emit(b); op(PDOP_NEG); fused(IADD, a); return; }
-        if (k == IDIV && L.ir[a].k == IC) { emit(b); opi(PDOP_RDIVC, L.ir[a].c); return; }
+        if (k == IDIV && L.ir[a].k == IC) { emit(b); opi(PDOP_RDIVC, L.ir[a].c, L.ir[a].lo); return; }
         if (k == IDIV && L.is_pvar(a)) { emit(b); op(PDOP_RDIV_P, parg(a)); return; }
         const int na = L.need(a), nb = L.need(b);
         static const int fwd[] = {0, 0, 0, 0, 0, 0, 0, 0, 0, PDOP_ADD, PDOP_SUB, PDOP_MUL, PDOP_DIV};

@@ -15,11 +15,13 @@
 
 #include "../../include/pdeval.h"
 #include "pdeval_kernels.h"
+#include "pdeval_point.h"
 #include "pdeval_tier2.h"
+#include "pdeval_launch.h"
 
 using namespace pd;
 
-#define PD_VERSION "pdeval 0.1 gfx950"
+#define PD_VERSION "pdeval 0.2 gfx950"
 
 // Work lists between the passes of one call (pdeval_pass_counts reports their sizes).
 enum {
@@ -31,7 +33,10 @@ enum {
     L_ESC_C = 5,      // tier-1 failures of the complex passes -> complex tier 2
     L_CPLX_DEEP = 6,  // complex stack 2 -> complex stack 8
     L_ESC_DEEP2 = 7,  // tier 2 stack 3 -> tier 2 stack 8
-    PD_N_LISTS = 8
+    L_PDEEP = 8,      // pass 0 -> deep point pass: real programs of stack 3..8
+    L_DD = 9,         // double-double point tier, real
+    L_DDC = 10,       // double-double point tier, complex
+    PD_N_LISTS = 11
 };
 
 struct pdeval_ctx {
@@ -41,6 +46,8 @@ struct pdeval_ctx {
     int fp_pts[PDEVAL_FP_N] = {0, 0, 0, 0};
     hipStream_t stream = nullptr;
     double ref_x[4] = {0, 0, 0, 0}, ref_y[4] = {0, 0, 0, 0};
+    dd ref_xd[4] = {}, ref_yd[4] = {};   // the reference points as double-doubles
+    dd kc_ref[16] = {};                  // Kerr operator coefficients there, double-double
     int nx = 0, ny = 0;
     double* d_gx = nullptr;   // nx grid abscissae
     double* d_gy = nullptr;   // ny grid ordinates
@@ -50,7 +57,8 @@ struct pdeval_ctx {
     // device work lists (capacity cap each) and their counters d_counts[L_*]
     int64_t* d_list[PD_N_LISTS] = {};
     int32_t* d_counts = nullptr;
-    uint8_t* d_pstate = nullptr;    // pass-0 point-stage state, capacity cap
+    uint8_t* d_pstate = nullptr;    // point-stage state, capacity cap
+    uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -65,9 +73,11 @@ struct pdeval_ctx {
     int ev_recorded = 0;
 };
 
+// in launch order (pass k lasts from event k to event k + 1)
 static const char* const kPassNames[PDEVAL_N_PASSES] = {
-    "pass0_point", "pass1_stack2", "pass2_stack3", "pass3_stack8", "complex_stack2", "complex_stack8",
-    "tier2_stack2", "tier2_stack3", "tier2_stack8", "tier2_complex"};
+    "pass0_point", "point_deep_complex", "pass1_stack2", "pass2_stack3", "pass3_stack8",
+    "complex_stack2", "complex_stack8", "tier2_stack2", "tier2_stack3", "tier2_stack8",
+    "tier2_complex", "point_dd"};
 
 static thread_local std::string g_err;
 
@@ -97,6 +107,23 @@ Grid default_grid(int problem) {
 
 // Kerr operator coefficients (kerr validator.py:69-91, M = 1, a = 1/10):
 // L[u] = G/(1-x^2) u_rr + G/Delta u_xx + d_r(G)/(1-x^2) u_r + d_x(G)/Delta u_x
+// in double-double at an exact rational point (the point stage's second tier)
+void kerr_coeffs_dd(dd r, dd x, dd* k) {
+    const dd M = dd_from(1.0), a = dd_ratio(1.0, 10.0);
+    const dd a2x2 = a * a * x * x;
+    const dd s = r * r + a2x2;
+    const dd s2 = s * s;
+    const dd G = dd_from(1.0) - dd_div(M * r * 2.0, s);
+    const dd Gr = dd_div(M * (r * r - a2x2) * 2.0, s2);
+    const dd Gx = dd_div(M * a * a * r * x * 4.0, s2);
+    const dd D = r * r - M * r * 2.0 + a * a;
+    const dd w = dd_from(1.0) - x * x;
+    k[0] = dd_div(G, w);
+    k[1] = dd_div(G, D);
+    k[2] = dd_div(Gr, w);
+    k[3] = dd_div(Gx, D);
+}
+
 void kerr_coeffs(double r_, double x_, double* k) {
     const long double M = 1.0L, a = 0.1L, r = r_, x = x_;
     const long double s = r * r + a * a * x * x;
@@ -141,19 +168,26 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
         return PDEVAL_ERR_ARG;
     }
     std::vector<double> px, py;
+    // the reference points as exact ratios (numerator, denominator)
+    std::vector<std::pair<double, double>> rx, ry;
     if (problem_id == PDEVAL_PROBLEM_FORCE_FREE) {
         // the paper's test point (rho, z) = (4/5, 6/7), validator.py:296-297
-        px = {0.8};
-        py = {6.0 / 7.0};
+        rx = {{4, 5}};
+        ry = {{6, 7}};
     } else {
         // kerr validator.py:167-171
-        px = {2.5, 7.0 / 3.0, 5.0};
-        py = {0.6, 1.0 / 3.0, -0.4};
+        rx = {{5, 2}, {7, 3}, {5, 1}};
+        ry = {{3, 5}, {1, 3}, {-2, 5}};
     }
-    c->n_ref = (int)px.size();
+    c->n_ref = (int)rx.size();
     for (int k = 0; k < c->n_ref; ++k) {
-        c->ref_x[k] = px[k];
-        c->ref_y[k] = py[k];
+        c->ref_xd[k] = dd_ratio(rx[k].first, rx[k].second);
+        c->ref_yd[k] = dd_ratio(ry[k].first, ry[k].second);
+        c->ref_x[k] = rx[k].first / rx[k].second;
+        c->ref_y[k] = ry[k].first / ry[k].second;
+        px.push_back(c->ref_x[k]);
+        py.push_back(c->ref_y[k]);
+        if (problem_id == PDEVAL_PROBLEM_KERR) kerr_coeffs_dd(c->ref_xd[k], c->ref_yd[k], &c->kc_ref[4 * k]);
     }
     std::vector<double> gx(nx), gy(ny);
     for (int i = 0; i < nx; ++i) gx[i] = g.x_lo + (i + g.x_ph) * ((g.x_hi - g.x_lo) / nx);
@@ -206,6 +240,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     for (int64_t* l : c->d_list)
         if (l) (void)hipFree(l);
     if (c->d_pstate) (void)hipFree(c->d_pstate);
+    if (c->d_status) (void)hipFree(c->d_status);
     for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) hipFree(p);
@@ -232,6 +267,8 @@ extern "C" int pdeval_default_params(int problem_id, pdeval_params* p) {
     p->strict_symbolic = 1;
     p->reserved = 0;
     p->noise_kappa = 16.0;  // true zeros <= 0.4, real residuals >= 1e8 x noise
+    p->point_abs_tol = 1e-20;  // validator.py:389
+    p->res_rel_acc = 1e-11;    // residuals reported to 1e-10 relative (BASELINE.json north star)
     (void)problem_id;
     return PDEVAL_OK;
 }
@@ -239,6 +276,11 @@ extern "C" int pdeval_default_params(int problem_id, pdeval_params* p) {
 // ---------------------------------------------------------------------------- program checks
 static int op_has_imm(uint32_t op) {
     return op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC || op == PDOP_POW;
+}
+// words taken by an opcode and its immediate(s) (PDEVAL_IMM_DD: a double-double low part too)
+static int op_words(int32_t w) {
+    if (!op_has_imm((uint32_t)w & 0xffu)) return 1;
+    return ((uint32_t)w & PDEVAL_IMM_DD) ? 5 : 3;
 }
 static int op_stack_delta(uint32_t op, int* need) {
     switch (op) {
@@ -261,16 +303,16 @@ extern "C" int pdeval_program_depth(const int32_t* ops, int64_t n_words) {
     for (int64_t pc = 1; pc < n_words;) {
         const uint32_t op = (uint32_t)ops[pc] & 0xffu;
         int need;
-        const int dd = op_stack_delta(op, &need);
+        const int delta = op_stack_delta(op, &need);
         if (need < 0) return -3;
         if (d < need) return -4;
         if (op == PDOP_POWN || (op >= PDOP_PUSH_P && op <= PDOP_RDIV_P)) {
             const int n = (ops[pc] >> 8) & 0xff;
             if (n < 2 || n > 16) return -5;
         }
-        d += dd;
+        d += delta;
         if (d > dmax) dmax = d;
-        pc += 1 + (op_has_imm(op) ? 2 : 0);
+        pc += op_words(ops[pc]);
         if (pc > n_words) return -6;
     }
     if (d != 1) return -7;
@@ -314,7 +356,7 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
             case PDOP_RDIV_P: f += 3 * (K + 1) + divf; break;
             default: break;
         }
-        pc += 1 + (op_has_imm(op) ? 2 : 0);
+        pc += op_words(ops[pc]);
     }
     // epilogue: force-free determinant + its magnitude shadow; Kerr 4-term operator + scale
     f += ff ? 2.0 * 160.0 : 16.0;
@@ -334,6 +376,9 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (c->d_pstate) (void)hipFree(c->d_pstate);
     c->d_pstate = nullptr;
     HIPCHK(c, hipMalloc(&c->d_pstate, cap));
+    if (c->d_status) (void)hipFree(c->d_status);
+    c->d_status = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_status, cap));
     c->cap = cap;
     return PDEVAL_OK;
 }
@@ -362,7 +407,10 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     for (int k = 0; k < 4; ++k) {
         a.ref_x[k] = c->ref_x[k];
         a.ref_y[k] = c->ref_y[k];
+        a.ref_xd[k] = c->ref_xd[k];
+        a.ref_yd[k] = c->ref_yd[k];
     }
+    for (int k = 0; k < 16; ++k) a.kc_ref[k] = c->kc_ref[k];
     a.gx = c->d_gx;
     a.gy = c->d_gy;
     a.nx = c->nx;
@@ -373,6 +421,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     for (int f = 0; f < PDEVAL_FP_N; ++f) a.fp_pts[f] = c->fp_pts[f];
     a.prm = prm;
     a.out = o;
+    // the double-double tier reads the final classes: keep them even if the caller does not
+    if (!a.out.status) a.out.status = c->d_status;
     a.list_capacity = c->cap;
     int32_t* const cnt = c->d_counts;
     HIPCHK(c, hipMemsetAsync(cnt, 0, PD_N_LISTS * sizeof(int32_t), s));
@@ -380,8 +430,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     constexpr bool FF = PROB == PDEVAL_PROBLEM_FORCE_FREE;
     constexpr int WPB = 4;  // waves (candidates) per 256-thread block of pass 1
     const int64_t blocks = (n + WPB - 1) / WPB;
-    // one list-driven pass: persistent one-wave blocks over list `in`, programs deeper than
-    // the variant's stack appended to `out`, tier-1 failures to `esc`
+    // one list-driven pass: persistent blocks over list `in`, programs deeper than the variant's
+    // stack appended to `out`, tier-1 failures to `esc`
     auto follow = [&](int in, int out, int esc) {
         KernelArgs b = a;
         b.list = c->d_list[in];
@@ -395,8 +445,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         return b;
     };
     const unsigned pgrid = (unsigned)std::min<int64_t>(4 * blocks, 8192);
-    // pass 1: programs whose stack fits 2 jets (92 % of force-free depth 4), one wave per
-    // candidate; deeper programs and complex-valued candidates go to device lists
+    // list-driven point kernels (one candidate per lane): enough blocks for the rare lists
+    const unsigned lgrid = (unsigned)std::min<int64_t>((n + 63) / 64, 2048);
     a.defer_list = c->d_list[L_DEFER];
     a.defer_count = cnt + L_DEFER;
     a.cplx_list = FF ? c->d_list[L_CPLX] : nullptr;
@@ -404,23 +454,41 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.esc_list = c->d_list[L_ESC];
     a.esc_count = cnt + L_ESC;
     a.pstate = c->d_pstate;
-    // pass 0: the point stage of every real candidate of stack <= 2, one candidate per lane
-    // (tier 1 + tier 2 at the reference points); complex-valued ones go to L_CPLX
+    a.pdeep_list = c->d_list[L_PDEEP];
+    a.pdeep_count = cnt + L_PDEEP;
+    // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
+    // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
+    // complex-valued ones -> L_CPLX
     mark(0);
     hipLaunchKernelGGL((point_kernel<PROB>), dim3((unsigned)((n + 255) / 256)), dim3(256),
                        (size_t)4 * 2 * nc(K) * 64 * sizeof(double), s, a);
     HIPCHK(c, hipGetLastError());
+    // the deep real programs, then (force-free) the complex list, operand stacks in private memory
     mark(1);
+    {
+        KernelArgs b = follow(L_PDEEP, -1, L_ESC);
+        launch_point_list(PROB, 0, lgrid, s, b);
+        HIPCHK(c, hipGetLastError());
+    }
+    if constexpr (FF) {
+        KernelArgs b = follow(L_CPLX, -1, L_ESC_C);
+        launch_point_list(PROB, 1, lgrid, s, b);
+        HIPCHK(c, hipGetLastError());
+    }
+    // ---- the grid stage
+    // pass 1: programs whose stack fits 2 jets (99 % of force-free depth 4), one wave per
+    // candidate; deeper programs go to L_DEFER, tier-1 grid failures to L_ESC
+    mark(2);
     hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256),
                        (stack_lds<double, K, 2>(4)), s, a);
     HIPCHK(c, hipGetLastError());
-    // pass 2: stack 3 (7 % of force-free depth 4; 2 LDS slots keep 10 waves per CU)
-    mark(2);
+    // pass 2: stack 3 (2 LDS slots keep 10 waves per CU)
+    mark(3);
     hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3(pgrid), dim3(64),
                        (stack_lds<double, K, 3>(1)), s, follow(L_DEFER, L_DEFER2, L_ESC));
     HIPCHK(c, hipGetLastError());
     // pass 3: stack 4..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
-    mark(3);
+    mark(4);
     hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
                        dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
                        (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
@@ -428,41 +496,60 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     if constexpr (FF) {
         // complex passes: candidates not real at the reference point, in complex arithmetic
         // (SymPy evaluates the point exactly, in the complex field: validator.py:363-402)
-        mark(4);
+        mark(5);
         hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3(pgrid), dim3(64),
                            (stack_lds<cplx, K, 2>(1)), s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C));
         HIPCHK(c, hipGetLastError());
-        mark(5);
+        mark(6);
         hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),
                            dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
                            (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
         HIPCHK(c, hipGetLastError());
     } else {
-        mark(4);
         mark(5);
+        mark(6);
     }
-    // tier 2 (pdeval_tier2.h): re-decide every tier-1 failure with error bounds, by stack depth
+    // tier 2 (pdeval_tier2.h): re-decide every tier-1 grid failure with error bounds, by stack
     KernelArgs t = follow(L_ESC, L_ESC_DEEP, L_ESC);
-    mark(6);
+    mark(7);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, 2>), dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(64),
                        (tier2_lds<double, K, 2>()), s, t);
     HIPCHK(c, hipGetLastError());
-    mark(7);
+    mark(8);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, 3>), dim3((unsigned)std::min<int64_t>(n, 4096)), dim3(64),
                        (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
     HIPCHK(c, hipGetLastError());
-    mark(8);
+    mark(9);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
                        dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, follow(L_ESC_DEEP2, -1, L_ESC));
     HIPCHK(c, hipGetLastError());
     if constexpr (FF) {
         // (complex programs deeper than 4 keep their tier-1 class: 161 KiB of LDS would not fit)
-        mark(9);
+        mark(10);
         hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4>), dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(64),
                            (tier2_lds<cplx, K, 4>()), s, follow(L_ESC_C, -1, L_ESC_C));
         HIPCHK(c, hipGetLastError());
     } else {
-        mark(9);
+        mark(10);
+    }
+    // ---- the point stage's double-double tier (pdeval_point.h): candidates fp64 left
+    // undecided, and provisional point passes whose grid stage rejected
+    mark(11);
+    {
+        KernelArgs b = a;
+        b.defer_list = c->d_list[L_DD];
+        b.defer_count = cnt + L_DD;
+        b.cplx_list = c->d_list[L_DDC];
+        b.cplx_count = cnt + L_DDC;
+        hipLaunchKernelGGL(dd_collect_kernel<PROB>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b,
+                           (const uint8_t*)a.out.status);
+        HIPCHK(c, hipGetLastError());
+        launch_dd_point(PROB, 0, lgrid, s, follow(L_DD, -1, L_ESC));
+        HIPCHK(c, hipGetLastError());
+        if constexpr (FF) {
+            launch_dd_point(PROB, 1, lgrid, s, follow(L_DDC, -1, L_ESC));
+            HIPCHK(c, hipGetLastError());
+        }
     }
     mark(PDEVAL_N_PASSES);
     c->ev_recorded = c->timing ? 1 : 0;
@@ -646,6 +733,65 @@ extern "C" int pdeval_eval_points(pdeval_ctx* c, const int32_t* prog, int64_t n_
     cleanup();
     if (e != hipSuccess) {
         c->err = std::string("pdeval_eval_points: ") + hipGetErrorString(e);
+        return PDEVAL_ERR_HIP;
+    }
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_point_states(pdeval_ctx* c, uint8_t* out, int64_t n) {
+    if (!c || !out || n < 0 || n > c->cap) {
+        if (c) c->err = "pdeval_point_states: bad argument";
+        return PDEVAL_ERR_ARG;
+    }
+    if (n == 0) return PDEVAL_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(out, c->d_pstate, n, hipMemcpyDeviceToHost));
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_point_eval(pdeval_ctx* c, const int32_t* prog, int64_t n_words, int tier, double* out,
+                                 uint8_t* state) {
+    if (!c || !prog || !out || !state || tier < 0 || tier > 3 ||
+        (c->problem == PDEVAL_PROBLEM_KERR && (tier & 1))) {
+        if (c) c->err = "pdeval_point_eval: bad argument";
+        return PDEVAL_ERR_ARG;
+    }
+    const int d = pdeval_program_depth(prog, n_words);
+    if (d < 0 || d > PDEVAL_MAX_STACK) {
+        c->err = "pdeval_point_eval: malformed program";
+        return PDEVAL_ERR_PROGRAM;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    pdeval_params prm;
+    pdeval_default_params(c->problem, &prm);
+    KernelArgs a{};
+    for (int k = 0; k < 4; ++k) {
+        a.ref_x[k] = c->ref_x[k];
+        a.ref_y[k] = c->ref_y[k];
+        a.ref_xd[k] = c->ref_xd[k];
+        a.ref_yd[k] = c->ref_yd[k];
+    }
+    for (int k = 0; k < 16; ++k) a.kc_ref[k] = c->kc_ref[k];
+    a.kc = c->d_kc;
+    a.n_ref = c->n_ref;
+    a.prm = prm;
+    int32_t* d_prog = nullptr;
+    double* d_out = nullptr;
+    uint8_t* d_st = nullptr;
+    hipError_t e = hipSuccess;
+    if ((e = hipMalloc(&d_prog, n_words * 4)) == hipSuccess && (e = hipMalloc(&d_out, 6 * 4 * 8)) == hipSuccess &&
+        (e = hipMalloc(&d_st, 1)) == hipSuccess &&
+        (e = hipMemcpy(d_prog, prog, n_words * 4, hipMemcpyHostToDevice)) == hipSuccess) {
+        launch_point_eval(c->problem, tier, c->stream, a, d_prog, (int)n_words, d_out, d_st);
+        if ((e = hipGetLastError()) == hipSuccess && (e = hipStreamSynchronize(c->stream)) == hipSuccess &&
+            (e = hipMemcpy(out, d_out, 6 * c->n_ref * 8, hipMemcpyDeviceToHost)) == hipSuccess)
+            e = hipMemcpy(state, d_st, 1, hipMemcpyDeviceToHost);
+    }
+    for (void* q : {(void*)d_prog, (void*)d_out, (void*)d_st})
+        if (q) (void)hipFree(q);
+    if (e != hipSuccess) {
+        c->err = std::string("pdeval_point_eval: ") + hipGetErrorString(e);
         return PDEVAL_ERR_HIP;
     }
     return PDEVAL_OK;

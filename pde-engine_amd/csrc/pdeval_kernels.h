@@ -15,6 +15,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/pdeval.h"
 #include "jet.h"
 
@@ -31,6 +33,8 @@ struct KernelArgs {
     // sample points: chunk 0 holds the reference points (lanes < n_ref), chunk c >= 1 the grid
     // row x = gx[(c-1) / (ny/64)] (one x per chunk: a scalar), y = gy[.. + lane]
     double ref_x[4], ref_y[4];
+    dd ref_xd[4], ref_yd[4];    // the same reference points as double-doubles (exact rationals)
+    dd kc_ref[16];              // Kerr: operator coefficients at the reference points, dd
     const double* gx;           // nx grid abscissae
     const double* gy;           // ny grid ordinates (ny % 64 == 0)
     int nx, ny;
@@ -47,7 +51,9 @@ struct KernelArgs {
     int64_t list_capacity;      // capacity of defer_list and cplx_list (appends beyond are dropped)
     int64_t* esc_list;          // tier-2 escalations: cand | ESC_* flags << 48
     int32_t* esc_count;
-    uint8_t* pstate;            // pass-0 point-stage state per candidate (P0_*), or NULL
+    uint8_t* pstate;            // point-stage state per candidate (P0_*), or NULL
+    int64_t* pdeep_list;        // real programs deeper than pass 0's stack: the deep point pass
+    int32_t* pdeep_count;
 };
 
 // Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).
@@ -58,8 +64,16 @@ enum : uint32_t {
     ESC_ANY_GRAD = 8,   // tier 1 saw a finite point with a non-zero gradient
     ESC_NFIN = 16,      // tier 1 saw at least one finite grid point
 };
-// Pass-0 point-stage state per candidate (point_kernel in pdeval_tier2.h)
-enum : uint8_t { P0_NONE = 0, P0_PASS = 1, P0_REJECT = 2, P0_CPLX = 3, P0_GRAD = 16 };
+// Point-stage state per candidate (pdeval_point.h).  Bits 0-1: P0_NONE (not decided: malformed
+// program, the grid pass runs its own chunk 0), P0_PASS, P0_REJECT (final).  Flags:
+//   P0_CPLX  not real at the reference point: the complex passes take the candidate
+//   P0_PROV  passed provisionally (|res| within kappa x fp64 noise): if the grid rejects, the
+//            double-double tier re-decides the point stage (REJECT_POINT vs REJECT_GRID)
+//   P0_GRAD  a reference point has a non-zero gradient
+//   P0_DD    undecided in fp64 (value too close to its noise or to a threshold): treated as
+//            PASS by the grid passes, decided by the double-double tier at the end
+enum : uint8_t { P0_NONE = 0, P0_PASS = 1, P0_REJECT = 2, P0_CPLX = 4, P0_PROV = 8, P0_GRAD = 16,
+                 P0_DD = 32 };
 
 #define PD_ESC_SHIFT 48
 #define PD_ESC_CAND_MASK ((1ll << PD_ESC_SHIFT) - 1)
@@ -77,6 +91,11 @@ __device__ __forceinline__ bool list_append(int64_t* list, int32_t* count, int64
 template <class T> struct Real;
 template <> struct Real<double> { static constexpr bool cplx_pass = false; };
 template <> struct Real<cplx> { static constexpr bool cplx_pass = true; };
+template <> struct Real<dd> { static constexpr bool cplx_pass = false; };
+template <> struct Real<cdd> { static constexpr bool cplx_pass = true; };
+template <class T> PD_HD T imag_unit();
+template <> PD_HD cplx imag_unit<cplx>() { return {0.0, 1.0}; }
+template <> PD_HD cdd imag_unit<cdd>() { return {{0.0, 0.0}, {1.0, 0.0}}; }
 
 // Program words are wave-uniform: read them through the constant address space so they
 // become scalar loads (s_load_dword, served by the scalar cache) instead of vector loads +
@@ -118,8 +137,9 @@ template <class T, int K> struct JetOps {
 #pragma unroll
         for (int i = 1; i < NC; ++i) t.c[i] = zero<T>();
     }
-    static PD_HD void set_var(J& t, double v, int axis) {
-        set_const(t, from_real<T>(v));
+    // coordinate operations take the coordinate as V = double, or dd in the double-double tier
+    template <class V> static PD_HD void set_var(J& t, V v, int axis) {
+        set_const(t, cvt<T>(v));
         t.c[axis == 0 ? ji(1, 0) : ji(0, 1)] = from_real<T>(1.0);
     }
     static PD_HD void add(const J& a, J& t) {
@@ -188,8 +208,8 @@ template <class T, int K> struct JetOps {
         for (int i = 0; i < NC; ++i) t.c[i] = t.c[i] * s;
     }
     // t *= (v + d_axis)
-    static PD_HD void mul_var(J& t, double v, int axis) {
-        const T vv = from_real<T>(v);
+    template <class V> static PD_HD void mul_var(J& t, V v, int axis) {
+        const T vv = cvt<T>(v);
 #pragma unroll
         for (int d = K; d >= 0; --d) {
 #pragma unroll
@@ -203,9 +223,9 @@ template <class T, int K> struct JetOps {
         }
     }
     // t /= (v + d_axis)
-    static PD_HD void div_var(J& t, double v, int axis) {
-        const T vv = from_real<T>(v);
-        const T inv = from_real<T>(1.0 / v);
+    template <class V> static PD_HD void div_var(J& t, V v, int axis) {
+        const T vv = cvt<T>(v);
+        const T inv = cvt<T>(rcp(v));
 #pragma unroll
         for (int d = 0; d <= K; ++d) {
 #pragma unroll
@@ -221,50 +241,50 @@ template <class T, int K> struct JetOps {
     // ---- coordinate powers p = v^n along an axis (PDOP_*_P): p_k = C(n,k) v^(n-k), k <= K.
     // Every index below is a compile-time constant after unrolling (axis is a template
     // parameter, n enters only through values), so the jets stay in registers.
-    template <int N> static PD_HD void pco_small(double v, double* pk) {   // N < K
-        double vp[N + 1];
-        vp[0] = 1.0;
+    template <int N, class V> static PD_HD void pco_small(V v, V* pk) {   // N < K
+        V vp[N + 1];
+        vp[0] = vone<V>();
 #pragma unroll
         for (int k = 1; k <= N; ++k) vp[k] = vp[k - 1] * v;
         double b = 1.0;
 #pragma unroll
         for (int k = 0; k <= K; ++k) {
-            pk[k] = k <= N ? b * vp[k <= N ? N - k : 0] : 0.0;
+            pk[k] = k <= N ? vp[k <= N ? N - k : 0] * b : vzero<V>();
             b = b * (double)(N - k) / (double)(k + 1);
         }
     }
-    static PD_HD void pcoefs(double v, int n, double* pk) {
+    template <class V> static PD_HD void pcoefs(V v, int n, V* pk) {
         if constexpr (K > 2) {
             if (n == 2) { pco_small<2>(v, pk); return; }
         }
         if constexpr (K > 3) {
             if (n == 3) { pco_small<3>(v, pk); return; }
         }
-        double base = 1.0;                  // v^(n-K), n >= K here
-        for (int e = 0; e < n - K; ++e) base *= v;
-        double pw[K + 1];
+        V base = vone<V>();                 // v^(n-K), n >= K here
+        for (int e = 0; e < n - K; ++e) base = base * v;
+        V pw[K + 1];
         pw[K] = base;
 #pragma unroll
         for (int k = K - 1; k >= 0; --k) pw[k] = pw[k + 1] * v;
         double b = 1.0;
 #pragma unroll
         for (int k = 0; k <= K; ++k) {
-            pk[k] = b * pw[k];
+            pk[k] = pw[k] * b;
             b = b * (double)(n - k) / (double)(k + 1);
         }
     }
     template <int AX> static PD_HD constexpr int pidx(int k, int other) { return AX == 0 ? ji(k, other) : ji(other, k); }
-    template <int AX> static PD_HD void set_p(J& t, const double* pk) {
-        set_const(t, from_real<T>(pk[0]));
+    template <int AX, class V> static PD_HD void set_p(J& t, const V* pk) {
+        set_const(t, cvt<T>(pk[0]));
 #pragma unroll
-        for (int k = 1; k <= K; ++k) t.c[pidx<AX>(k, 0)] = from_real<T>(pk[k]);
+        for (int k = 1; k <= K; ++k) t.c[pidx<AX>(k, 0)] = cvt<T>(pk[k]);
     }
-    template <int AX> static PD_HD void add_p(J& t, const double* pk, double sg) {
+    template <int AX, class V> static PD_HD void add_p(J& t, const V* pk, double sg) {
 #pragma unroll
-        for (int k = 0; k <= K; ++k) t.c[pidx<AX>(k, 0)] = t.c[pidx<AX>(k, 0)] + from_real<T>(sg * pk[k]);
+        for (int k = 0; k <= K; ++k) t.c[pidx<AX>(k, 0)] = t.c[pidx<AX>(k, 0)] + cvt<T>(pk[k] * sg);
     }
     // t *= p in place (decreasing degree: c_ij reads t at lower orders along the axis)
-    template <int AX> static PD_HD void mul_p(J& t, const double* pk) {
+    template <int AX, class V> static PD_HD void mul_p(J& t, const V* pk) {
 #pragma unroll
         for (int d = K; d >= 0; --d) {
 #pragma unroll
@@ -274,15 +294,15 @@ template <class T, int K> struct JetOps {
                 T s = t.c[ji(i, j)] * pk[0];
 #pragma unroll
                 for (int k = 1; k <= K; ++k)
-                    if (k <= ia) s = fmac(t.c[pidx<AX>(ia - k, io)], from_real<T>(pk[k]), s);
+                    if (k <= ia) s = fmac(t.c[pidx<AX>(ia - k, io)], cvt<T>(pk[k]), s);
                 t.c[ji(i, j)] = s;
             }
         }
     }
     // t /= p in place (increasing degree)
-    template <int AX> static PD_HD void div_p(J& t, const double* pk) {
-        const T b0 = from_real<T>(pk[0]);
-        const T inv = from_real<T>(1.0 / pk[0]);
+    template <int AX, class V> static PD_HD void div_p(J& t, const V* pk) {
+        const T b0 = cvt<T>(pk[0]);
+        const T inv = cvt<T>(rcp(pk[0]));
 #pragma unroll
         for (int d = 0; d <= K; ++d) {
 #pragma unroll
@@ -292,13 +312,13 @@ template <class T, int K> struct JetOps {
                 T s = t.c[ji(i, j)];
 #pragma unroll
                 for (int k = 1; k <= K; ++k)
-                    if (k <= ia) s = fmac(t.c[pidx<AX>(ia - k, io)], from_real<T>(-pk[k]), s);
+                    if (k <= ia) s = fmac(t.c[pidx<AX>(ia - k, io)], cvt<T>(-pk[k]), s);
                 t.c[ji(i, j)] = qdiv(s, b0, inv);
             }
         }
     }
     // the opcode's action on the top of stack for a fixed axis
-    template <int AX> static PD_HD void p_op(uint32_t op, J& t, const double* pk) {
+    template <int AX, class V> static PD_HD void p_op(uint32_t op, J& t, const V* pk) {
         if (op == PDOP_ADD_P) add_p<AX>(t, pk, 1.0);
         else if (op == PDOP_SUB_P) add_p<AX>(t, pk, -1.0);
         else if (op == PDOP_MUL_P) mul_p<AX>(t, pk);
@@ -377,7 +397,7 @@ template <class T, int K> struct JetOps {
         T f[K + 1];
         f[0] = exp_(t.c[0]);
 #pragma unroll
-        for (int k = 1; k <= K; ++k) f[k] = f[k - 1] * (1.0 / k);
+        for (int k = 1; k <= K; ++k) f[k] = divk(f[k - 1], 1.0, k);
         jcompose<T, K>(t.c, f);
     }
     static PD_HD void logj(J& t) {
@@ -387,7 +407,7 @@ template <class T, int K> struct JetOps {
         T rk = r;
 #pragma unroll
         for (int k = 1; k <= K; ++k) {
-            f[k] = rk * (((k & 1) ? 1.0 : -1.0) / k);
+            f[k] = divk(rk, (k & 1) ? 1.0 : -1.0, k);
             rk = rk * r;
         }
         jcompose<T, K>(t.c, f);
@@ -403,6 +423,14 @@ template <int K> __device__ __forceinline__ void absj(typename JetOps<cplx, K>::
     // Abs of a complex value is not holomorphic: only real arguments are meaningful
     const double s = (t.c[0].im == 0.0) ? (t.c[0].re > 0.0 ? 1.0 : (t.c[0].re < 0.0 ? -1.0 : NAN)) : NAN;
     JetOps<cplx, K>::scale(t, from_real<cplx>(s));
+}
+template <int K> __device__ __forceinline__ void absj(typename JetOps<dd, K>::J& t) {
+    const double s = t.c[0].hi > 0.0 ? 1.0 : (t.c[0].hi < 0.0 ? -1.0 : NAN);
+    JetOps<dd, K>::scale(t, from_real<dd>(s));
+}
+template <int K> __device__ __forceinline__ void absj(typename JetOps<cdd, K>::J& t) {
+    const double s = is_zero(t.c[0].im) ? (t.c[0].re.hi > 0.0 ? 1.0 : (t.c[0].re.hi < 0.0 ? -1.0 : NAN)) : NAN;
+    JetOps<cdd, K>::scale(t, from_real<cdd>(s));
 }
 
 // ------------------------------------------------------------------ residual epilogues
@@ -453,10 +481,11 @@ template <class T, bool MAG> struct FFEpi {
         out[ji(0, 1)] = fmac(q00, fr01, q01 * fr00) + sgn(fmac(p00, fz01, p01 * fz00));
     }
 
-    static PD_HD T eval(const T* u, double rho) {
-        const double r0 = 1.0 / rho;
+    // rho: R = double, or dd in the double-double point tier
+    template <class R> static PD_HD T eval(const T* u, R rho) {
+        const R r0 = rcp(rho);
         // 1/rho jet in the rho direction: (-1)^i / rho^(i+1)
-        const double ri[3] = {r0, (MAG ? 1.0 : -1.0) * r0 * r0, r0 * r0 * r0};
+        const R ri[3] = {r0, r0 * r0 * (MAG ? 1.0 : -1.0), r0 * r0 * r0};
         T LA[3], LB[3];
         {
             // A = p_rho + q_z - p / rho   (validator.py:323), order 2
@@ -470,7 +499,7 @@ template <class T, bool MAG> struct FFEpi {
                     s = fmac(U(u, i, j + 2), from_real<T>((double)((j + 1) * (j + 2))), s);
                     T pr = P(u, i, j) * ri[0];
 #pragma unroll
-                    for (int i1 = 1; i1 <= i; ++i1) pr = fmac(P(u, i - i1, j), from_real<T>(ri[i1]), pr);
+                    for (int i1 = 1; i1 <= i; ++i1) pr = fmac(P(u, i - i1, j), cvt<T>(ri[i1]), pr);
                     A[ji(i, j)] = s + sgn(pr);
                 }
             lie1(u, A, LA);
@@ -645,9 +674,9 @@ template <class T, int K, int MAXD> struct Interp {
             double imm = 0.0;
             int npc = pc + 1;
             if (op_has_imm(op)) {
-                if (pc + 3 > end) return RUN_BAD;
+                npc = pc + ((w & PDEVAL_IMM_DD) ? 5 : 3);   // (the double-double low part is skipped)
+                if (npc > end) return RUN_BAD;
                 imm = rd_imm(ops + pc + 1);
-                npc = pc + 3;
             }
             const uint32_t wn = (npc < end) ? rd_word(ops + npc) : 0u;
             switch (op) {
@@ -792,11 +821,11 @@ void validate_kernel(KernelArgs a) {
         if ((hdr & 0xffu) != 0u) status = PDEVAL_CLS_BAD_PROGRAM;
         // pass 0 decided the point stage of most real candidates (P0_*)
         uint8_t ps = P0_NONE;
+        if (a.pstate) ps = (uint8_t)__builtin_amdgcn_readfirstlane((int)a.pstate[cand]);
         if constexpr (!Real<T>::cplx_pass) {
-            if (a.pstate) ps = (uint8_t)__builtin_amdgcn_readfirstlane((int)a.pstate[cand]);
+            if (ps & P0_CPLX) continue;                            // the complex passes take it
         }
-        if ((ps & 3) == P0_CPLX) continue;                        // the complex pass takes it
-        if ((ps & 3) == P0_REJECT && !a.prm.full_grid) continue;  // final after pass 0
+        if ((ps & 3) == P0_REJECT && !a.prm.full_grid) continue;  // final after the point stage
         const bool p0 = (ps & 3) != P0_NONE;
         if constexpr (!Real<T>::cplx_pass) {
             if (status < 0 && !p0 && (hdr & PDEVAL_FLAG_COMPLEX)) {

@@ -1,0 +1,375 @@
+// pdeval_point.h -- the point stage: the reference's first verdict stage, decided for every
+// candidate before the grid passes run.
+//
+// The reference evaluates its residual EXACTLY at its test point(s):
+//   force-free  det at (rho, z) = (4/5, 6/7): reject when cancel(together(det)) is a non-zero
+//               Number ("Invalid (point check != 0)") or when |evalf(50)| >= 1e-20 ("Invalid
+//               (point check ~ x.xxe+yy)"), pass otherwise      (problems/force_free/validator.py:349-402)
+//   Kerr        lhs at (5/2, 3/5), (7/3, 1/3), (5, -2/5), N(., 40): reject when non-real or when
+//               max |lhs| >= 1e-10 (absolute)                   (kerr_magnetosphere/validator.py:163-192)
+// Here every reference point is evaluated with the error-bounded interpreter (pdeval_tier2.h),
+// which carries a first-order bound `noise` of the rounding error beside the value:
+//   tier A (fp64): decide where the bound makes the answer certain and the value accurate to
+//           res_rel_acc (1e-11, so the reported residual is within 1e-10 of the exact one);
+//           where |res| <= kappa*noise the point passes PROVISIONALLY (P0_PROV): the exact value
+//           may be 0 (a true solution) or a non-zero hidden in fp64 noise;
+//   tier B (double-double, dd.h, at the end of the call): the undecided candidates (P0_DD) and
+//           the provisional passes whose grid stage rejected -- exactly the candidates whose
+//           class (REJECT_POINT vs REJECT_GRID) depends on the hidden value -- are re-evaluated
+//           with ~106-bit arithmetic, reference points and constants as double-doubles, and
+//           decided for good (noise unit 2^-100).
+// A provisional pass whose grid stage accepts is not re-evaluated: a determinant that vanishes
+// on the whole grid is identically zero (analytic), so it vanishes exactly at p* as well.
+// Kernels (launch order in pdeval.hip):
+//   point_kernel         pass 0: all candidates of stack <= 2, real, one candidate per lane
+//   point_list_kernel    deeper real programs (list), then the complex candidates (list)
+//   dd_collect_kernel    builds the tier-B lists from pstate and the final classes
+//   dd_point_kernel      tier B, real (dd) and complex (cdd) lists
+#pragma once
+#include "pdeval_tier2.h"
+
+namespace pd {
+
+PD_HD double re_hi(double v) { return v; }
+PD_HD double re_hi(cplx v) { return v.re; }
+PD_HD double re_hi(dd v) { return v.hi; }
+PD_HD double re_hi(cdd v) { return v.re.hi; }
+PD_HD double im_hi(double) { return 0.0; }
+PD_HD double im_hi(cplx v) { return v.im; }
+PD_HD double im_hi(dd) { return 0.0; }
+PD_HD double im_hi(cdd v) { return v.im.hi; }
+
+// reference point k (uniform within the loop over points) as the coordinate type V
+template <class V> __device__ __forceinline__ V ref_coord(const KernelArgs& a, int k, int axis);
+template <> __device__ __forceinline__ double ref_coord<double>(const KernelArgs& a, int k, int axis) {
+    const double* t = axis ? a.ref_y : a.ref_x;
+    return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3]));
+}
+template <> __device__ __forceinline__ dd ref_coord<dd>(const KernelArgs& a, int k, int axis) {
+    const dd* t = axis ? a.ref_yd : a.ref_xd;
+    return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3]));
+}
+
+struct PtEval {
+    double res_re, res_im, res_abs;  // residual (hi parts)
+    double S, noise;                 // magnitude scale and first-order noise bound
+    double u0;                       // Re u at the point (fingerprint)
+    bool finite, grad_zero;
+    int rc;                          // RUN_*
+};
+
+// Kerr operator with coefficients of type KC (double table or dd at the reference points)
+template <class T, class KC> __device__ __forceinline__ T kerr_lhs(const T* u, const KC* k, double* S) {
+    const T t1 = u[ji(2, 0)] * cvt<T>(k[0] * 2.0);
+    const T t2 = u[ji(0, 2)] * cvt<T>(k[1] * 2.0);
+    const T t3 = u[ji(1, 0)] * cvt<T>(k[2]);
+    const T t4 = u[ji(0, 1)] * cvt<T>(k[3]);
+    *S = (mag(t1) + mag(t2)) + (mag(t3) + mag(t4));
+    return (t1 + t2) + (t3 + t4);
+}
+
+// Value and noise bound of one program at reference point k.
+template <int PROB, class T, class V, int MAXD, bool VEC, class STK>
+__device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t* prog, int plen, int k,
+                                             STK& stk) {
+    constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    constexpr int NC = nc(K);
+    using EI = ErrInterp<T, K, MAXD, V>;
+    PtEval r{};
+    const V x = ref_coord<V>(a, k, 0), y = ref_coord<V>(a, k, 1);
+    typename EI::J u;
+    double e[NC];
+    // the reference points are rounded to the coordinate type: half a unit of fp64, ~2^-7 of the
+    // double-double noise unit (dd_unit = 2^-100 against a rounding of 2^-107)
+    const double cerr = std::is_same<V, dd>::value ? 0x1p-6 : 0.5;
+    r.rc = EI::template run_s<VEC>(prog, 1, plen, x, y, u, e, stk, cerr);
+    if (r.rc != RUN_OK) return r;
+    double m[NC];
+#pragma unroll
+    for (int i = 0; i < NC; ++i) m[i] = mag(u.c[i]);
+    const double* kc = a.kc ? a.kc + 4 * k : nullptr;
+    T res;
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+        res = FFEpi<T, false>::eval(u.c, x);
+        r.S = FFEpi<double, true>::eval(m, hi_of(x));
+    } else {
+        if constexpr (std::is_same<V, dd>::value) res = kerr_lhs<T, dd>(u.c, a.kc_ref + 4 * k, &r.S);
+        else res = kerr_lhs<T, double>(u.c, kc, &r.S);
+    }
+    const double unit = std::is_same<V, dd>::value ? dd_unit() / kEps : 1.0;
+    r.noise = residual_noise<PROB, T>(u.c, e, hi_of(x), kc, r.S) * unit;
+    r.res_re = re_hi(res);
+    r.res_im = im_hi(res);
+    r.res_abs = mag(res);
+    r.u0 = re_hi(u.c[0]);
+    r.grad_zero = is_zero(u.c[ji(1, 0)]) && is_zero(u.c[ji(0, 1)]);
+    bool fin = finite_(res) && isfinite(r.S) && isfinite(r.noise);
+#pragma unroll
+    for (int i = 0; i < NC; ++i) fin = fin && m[i] < kHugeJet;
+    r.finite = fin;
+    return r;
+}
+
+// ---- decision rules.  FINAL = the double-double tier (nothing is left undecided).
+// Force-free (validator.py:371-397): returns P0_PASS / P0_REJECT, | P0_PROV, | P0_DD.
+// P0_DD alone with P0_PASS: the class is undecided in fp64 (the grid passes treat it as passed);
+// P0_DD with a decided class: only the reported residual needs the double-double value.
+template <bool FINAL>
+__device__ __forceinline__ uint8_t ff_point_rule(double res_abs, double noise, bool rational,
+                                                 const pdeval_params& prm) {
+    const double kn = prm.noise_kappa * noise;
+    if (res_abs > kn) {                                    // certainly non-zero
+        const uint8_t acc = (!FINAL && kn > prm.res_rel_acc * res_abs) ? P0_DD : 0;
+        if (rational) return P0_REJECT | acc;             // an exact Number != 0
+        if (res_abs - kn >= prm.point_abs_tol) return P0_REJECT | acc;   // |evalf(50)| >= 1e-20
+        if (res_abs + kn < prm.point_abs_tol) return P0_PASS | acc;      // non-zero below 1e-20
+        if (!FINAL) return P0_DD | P0_PASS;
+        return res_abs >= prm.point_abs_tol ? P0_REJECT : P0_PASS;
+    }
+    return FINAL ? P0_PASS : (uint8_t)(P0_PASS | P0_PROV);
+}
+
+// Kerr, one reference point (kerr validator.py:190, absolute tolerance): 0 pass, 1 reject,
+// 2 undecided in fp64; | 4: the value is not accurate enough to report (double-double value).
+template <bool FINAL>
+__device__ __forceinline__ int kerr_point_rule(double res_abs, double noise, const pdeval_params& prm) {
+    const double kn = prm.noise_kappa * noise;
+    if (FINAL) return res_abs >= prm.kerr_abs_tol ? 1 : 0;
+    const int acc = (res_abs > kn && kn > prm.res_rel_acc * res_abs) ? 4 : 0;
+    if (res_abs - kn >= prm.kerr_abs_tol) return 1 | acc;
+    if (res_abs + kn < prm.kerr_abs_tol) return 0 | acc;
+    return 2;
+}
+
+// The point stage of one candidate (per lane).  Returns the P0_* state; writes q_ref, res_ref and
+// the fingerprint of point 0.  *nonfinite: some reference point is not finite (force-free real
+// pass: the complex pass takes the candidate).
+template <int PROB, class T, class V, int MAXD, bool VEC, bool FINAL, class STK>
+__device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand, const int32_t* prog, int plen,
+                                               uint32_t hdr, STK& stk, bool* nonfinite, bool* prog_err) {
+    double qr = 0.0;
+    bool nf = false, grad = false, rej = false, und = false, inacc = false;
+    uint8_t ff = P0_PASS;
+    *prog_err = false;
+    for (int p = 0; p < a.n_ref; ++p) {
+        const PtEval r = point_eval<PROB, T, V, MAXD, VEC>(a, prog, plen, p, stk);
+        if (r.rc != RUN_OK) {
+            *prog_err = true;
+            return P0_NONE;
+        }
+        if (p == 0 && a.out.fingerprint) a.out.fingerprint[cand * PDEVAL_FP_N] = r.u0;
+        // (a complex residual: its modulus with the sign of its real part)
+        if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = r.res_im == 0.0 ? r.res_re : copysign(r.res_abs, r.res_re);
+        if (!r.finite) {
+            nf = true;
+            // finite, but a coefficient beyond the 2^160 guard: a sure reject whose value the
+            // double-double tier still reports accurately
+            if (!FINAL && isfinite(r.res_abs) && isfinite(r.S)) inacc = true;
+            continue;
+        }
+        if (!r.grad_zero) grad = true;
+        if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+            qr = scaled(r.res_abs, r.S);
+            ff = ff_point_rule<FINAL>(r.res_abs, r.noise, (hdr & PDEVAL_FLAG_RATIONAL) != 0, a.prm);
+        } else {
+            qr = fmax(qr, r.res_abs);
+            const int k = kerr_point_rule<FINAL>(r.res_abs, r.noise, a.prm);
+            rej = rej || (k & 3) == 1;
+            und = und || (k & 3) == 2;
+            inacc = inacc || (k & 4);
+        }
+    }
+    *nonfinite = nf;
+    if (a.out.q_ref) a.out.q_ref[cand] = qr;
+    uint8_t ps;
+    if (nf) ps = P0_REJECT;    // Kerr: non-real / NaN at a test point; FF complex: not finite
+    else if (PROB == PDEVAL_PROBLEM_FORCE_FREE) ps = ff;
+    else ps = und ? (uint8_t)(P0_DD | P0_PASS) : (rej ? P0_REJECT : P0_PASS);
+    if (inacc) ps |= P0_DD;
+    if (grad) ps |= P0_GRAD;
+    return ps;
+}
+
+// A point reject is final: with full_grid = 0 the grid passes skip the candidate (the
+// reference's control flow), so its outputs are written here.
+__device__ __forceinline__ void write_point_reject(const KernelArgs& a, int64_t cand) {
+    if (a.out.status) a.out.status[cand] = PDEVAL_CLS_REJECT_POINT;
+    if (!a.prm.full_grid) {
+        if (a.out.q_grid) a.out.q_grid[cand] = 0.0;
+        if (a.out.n_bad) a.out.n_bad[cand] = 0;
+        if (a.out.n_nonfinite) a.out.n_nonfinite[cand] = 0;
+    }
+}
+
+__device__ __forceinline__ bool prog_bounds(const KernelArgs& a, int64_t cand, int64_t* beg, int64_t* end) {
+    *beg = a.offsets[cand];
+    *end = a.offsets[cand + 1];
+    return *beg >= 0 && *end > *beg && *end <= a.n_words && *end - *beg < (1 << 24);
+}
+
+// Pass 0: every candidate, one per LANE (the lanes of a wave interpret different programs: a
+// divergent dispatch, still ~64x the lane use of a wave per candidate at one point).  Real
+// programs of stack <= 2 are decided here (operand stack in LDS); deeper ones go to the deep
+// point pass, complex-valued ones (FF) to the complex list.
+template <int PROB>
+__global__ __launch_bounds__(256, 1) void point_kernel(KernelArgs a) {
+    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
+    constexpr int NC = nc(K);
+    constexpr int MAXD = 2;
+    const int lane = threadIdx.x & 63;
+    const int wib = threadIdx.x >> 6;
+#ifndef PD_HOST_SIM
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
+    double* vs = reinterpret_cast<double*>(pd_lds) + (size_t)wib * 2 * (MAXD - 1) * NC * 64;
+    double* es = vs + (size_t)(MAXD - 1) * NC * 64;
+    LdsStack<double, NC> stk{vs, es, lane};
+    const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cand >= a.n) return;
+    int64_t beg, end;
+    uint8_t ps = P0_NONE;
+    if (prog_bounds(a, cand, &beg, &end)) {
+        const int32_t* prog = a.ops + beg;
+        const uint32_t hdr = (uint32_t)prog[0];
+        const int depth = (int)((hdr >> 8) & 0xffu);
+        if ((hdr & 0xffu) == 0u && depth <= PDEVAL_MAX_STACK) {
+            if (hdr & PDEVAL_FLAG_COMPLEX) {
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+                    if (a.cplx_list && list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand)) ps = P0_CPLX;
+                } else {
+                    ps = P0_REJECT;          // Kerr: non-real at a test point (kerr validator.py:179-180)
+                }
+            } else if (depth > MAXD) {
+                if (a.pdeep_list) list_append(a.pdeep_list, a.pdeep_count, a.list_capacity, cand);
+            } else {
+                bool nf, perr;
+                const uint8_t s = point_stage<PROB, double, double, MAXD, true, false>(
+                    a, cand, prog, (int)(end - beg), hdr, stk, &nf, &perr);
+                if (!perr) {
+                    if (nf && PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+                        // not real at p*: the complex passes decide (SymPy evaluates the point
+                        // exactly, in the complex field: validator.py:363-402)
+                        if (a.cplx_list && list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand))
+                            ps = P0_CPLX;
+                    } else {
+                        ps = s;
+                    }
+                }
+            }
+        }
+    }
+    a.pstate[cand] = ps;
+    if ((ps & 3) == P0_REJECT) write_point_reject(a, cand);
+}
+
+// The point stage over a device list, one candidate per lane, operand stack in private memory:
+// T = double for the real programs deeper than pass 0 takes, T = cplx for the complex list.
+template <int PROB, class T>
+__global__ __launch_bounds__(64, 1) void point_list_kernel(KernelArgs a) {
+    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
+    constexpr int MAXD = PDEVAL_MAX_STACK;
+    int64_t nwork = (int64_t)(*a.list_count);
+    if (nwork > a.list_capacity) nwork = a.list_capacity;
+    PrivStack<T, nc(K), MAXD - 1> stk;
+    for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwork;
+         wi += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t cand = a.list[wi];
+        int64_t beg, end;
+        if (!prog_bounds(a, cand, &beg, &end)) continue;   // pass 0 checked these
+        const int32_t* prog = a.ops + beg;
+        const uint32_t hdr = (uint32_t)prog[0];
+        bool nf, perr;
+        uint8_t s = point_stage<PROB, T, double, MAXD, true, false>(a, cand, prog, (int)(end - beg), hdr, stk,
+                                                                   &nf, &perr);
+        uint8_t ps = P0_NONE;
+        if (!perr) {
+            if constexpr (Real<T>::cplx_pass) {
+                ps = (uint8_t)(s | P0_CPLX);   // not finite even in the complex field: reject
+            } else {
+                if (nf && PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+                    if (a.cplx_list && list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand)) ps = P0_CPLX;
+                } else {
+                    ps = s;
+                }
+            }
+        } else if constexpr (Real<T>::cplx_pass) {
+            ps = P0_CPLX;   // malformed: the complex grid pass classifies it (chunk 0)
+        }
+        a.pstate[cand] = ps;
+        if ((ps & 3) == P0_REJECT) write_point_reject(a, cand);
+    }
+}
+
+// Tier-B lists: the candidates whose point stage fp64 left undecided, and the provisional
+// passes whose final class is a grid reject (that class may really be a point reject).
+template <int PROB>
+__global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a, const uint8_t* status) {
+    const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cand >= a.n) return;
+    const uint8_t ps = a.pstate[cand];
+    if ((ps & 3) == P0_NONE) return;
+    const uint8_t st = status[cand];
+    const bool need = (ps & P0_DD) ||
+                      ((ps & P0_PROV) && (st == PDEVAL_CLS_REJECT_GRID || st == PDEVAL_CLS_REJECT_SYMBOLIC));
+    if (!need) return;
+    if (ps & P0_CPLX) list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
+    else list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
+}
+
+// Tier B: the point stage in double-double (T = dd, or cdd for complex candidates), final.
+template <int PROB, class T>
+__global__ __launch_bounds__(64, 1) void dd_point_kernel(KernelArgs a) {
+    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
+    constexpr int MAXD = PDEVAL_MAX_STACK;
+    int64_t nwork = (int64_t)(*a.list_count);
+    if (nwork > a.list_capacity) nwork = a.list_capacity;
+    PrivStack<T, nc(K), MAXD - 1> stk;
+    for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwork;
+         wi += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t cand = a.list[wi];
+        int64_t beg, end;
+        if (!prog_bounds(a, cand, &beg, &end)) continue;
+        const int32_t* prog = a.ops + beg;
+        const uint32_t hdr = (uint32_t)prog[0];
+        bool nf, perr;
+        const uint8_t s = point_stage<PROB, T, dd, MAXD, true, true>(a, cand, prog, (int)(end - beg), hdr, stk,
+                                                                    &nf, &perr);
+        if (perr || nf) continue;   // (finite in fp64: keep the fp64 decision)
+        const uint8_t st = a.out.status ? a.out.status[cand] : (uint8_t)PDEVAL_CLS_ACCEPT;
+        // the reference checks the gradient (and Kerr the constant) before the point stage
+        const bool overridable = st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||
+                                 st == PDEVAL_CLS_REJECT_SYMBOLIC;
+        if ((s & 3) == P0_REJECT && overridable) {
+            write_point_reject(a, cand);
+            if (a.out.verdict_bits)
+                atomicAnd((uint32_t*)a.out.verdict_bits + (cand >> 5), ~(1u << (cand & 31)));
+        }
+        a.pstate[cand] = (uint8_t)((a.pstate[cand] & ~(3 | P0_DD | P0_PROV)) | (s & 3));
+    }
+}
+
+// Diagnostic (pdeval_point_eval): one program at every reference point in one precision
+// tier, one lane per point; out[6 k ..] = {res_re, res_im, |res|, S, noise, finite (1/0, -1 =
+// program error)}; states[0] = the point-stage decision of the tier (P0_* of point_stage).
+template <int PROB, class T, class V, bool FINAL>
+__global__ __launch_bounds__(64, 1) void point_eval_kernel(KernelArgs a, const int32_t* prog, int plen,
+                                                           double* out, uint8_t* states) {
+    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
+    PrivStack<T, nc(K), PDEVAL_MAX_STACK - 1> stk;
+    const int k = threadIdx.x;
+    if (k < a.n_ref) {
+        const PtEval r = point_eval<PROB, T, V, PDEVAL_MAX_STACK, true>(a, prog, plen, k, stk);
+        double* o = out + 6 * k;
+        o[0] = r.res_re; o[1] = r.res_im; o[2] = r.res_abs; o[3] = r.S; o[4] = r.noise;
+        o[5] = r.rc ? -1.0 : (r.finite ? 1.0 : 0.0);
+    }
+    if (k == 0) {
+        bool nf, perr;
+        states[0] = point_stage<PROB, T, V, PDEVAL_MAX_STACK, true, FINAL>(a, 0, prog, plen, (uint32_t)prog[0], stk,
+                                                                         &nf, &perr);
+    }
+}
+
+}  // namespace pd

@@ -1,0 +1,42 @@
+// pdeval_point.hip -- the rare point-stage kernels (pdeval_point.h) in their own translation
+// unit: the deep / complex list passes and the double-double tier.
+#include <hip/hip_runtime.h>
+
+#include "pdeval_launch.h"
+#include "pdeval_point.h"
+
+namespace pd {
+
+void launch_point_list(int problem, int cplx, unsigned grid, hipStream_t s, const KernelArgs& a) {
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+        if (cplx) hipLaunchKernelGGL((point_list_kernel<PDEVAL_PROBLEM_FORCE_FREE, pd::cplx>), dim3(grid), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((point_list_kernel<PDEVAL_PROBLEM_FORCE_FREE, double>), dim3(grid), dim3(64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((point_list_kernel<PDEVAL_PROBLEM_KERR, double>), dim3(grid), dim3(64), 0, s, a);
+    }
+}
+
+void launch_dd_point(int problem, int cplx, unsigned grid, hipStream_t s, const KernelArgs& a) {
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+        if (cplx) hipLaunchKernelGGL((dd_point_kernel<PDEVAL_PROBLEM_FORCE_FREE, cdd>), dim3(grid), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((dd_point_kernel<PDEVAL_PROBLEM_FORCE_FREE, dd>), dim3(grid), dim3(64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL((dd_point_kernel<PDEVAL_PROBLEM_KERR, dd>), dim3(grid), dim3(64), 0, s, a);
+    }
+}
+
+void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a, const int32_t* prog, int plen,
+                       double* out, uint8_t* state) {
+    constexpr int FF = PDEVAL_PROBLEM_FORCE_FREE, KR = PDEVAL_PROBLEM_KERR;
+    if (problem == FF) {
+        if (tier == 0) hipLaunchKernelGGL((point_eval_kernel<FF, double, double, false>), dim3(1), dim3(64), 0, s, a, prog, plen, out, state);
+        else if (tier == 1) hipLaunchKernelGGL((point_eval_kernel<FF, pd::cplx, double, false>), dim3(1), dim3(64), 0, s, a, prog, plen, out, state);
+        else if (tier == 2) hipLaunchKernelGGL((point_eval_kernel<FF, dd, dd, true>), dim3(1), dim3(64), 0, s, a, prog, plen, out, state);
+        else hipLaunchKernelGGL((point_eval_kernel<FF, cdd, dd, true>), dim3(1), dim3(64), 0, s, a, prog, plen, out, state);
+    } else {
+        if (tier == 0) hipLaunchKernelGGL((point_eval_kernel<KR, double, double, false>), dim3(1), dim3(64), 0, s, a, prog, plen, out, state);
+        else hipLaunchKernelGGL((point_eval_kernel<KR, dd, dd, true>), dim3(1), dim3(64), 0, s, a, prog, plen, out, state);
+    }
+}
+
+}  // namespace pd

@@ -69,14 +69,14 @@ template <class T, int K> __device__ __forceinline__ void outer_coefs(uint32_t o
     if (op == PDOP_EXP) {
         f[0] = exp_(x0);
 #pragma unroll
-        for (int k = 1; k <= K + 1; ++k) f[k] = f[k - 1] * (1.0 / k);
+        for (int k = 1; k <= K + 1; ++k) f[k] = divk(f[k - 1], 1.0, k);
     } else if (op == PDOP_LOG) {
         const T r = recip(x0);
         f[0] = log_(x0);
         T rk = r;
 #pragma unroll
         for (int k = 1; k <= K + 1; ++k) {
-            f[k] = rk * (((k & 1) ? 1.0 : -1.0) / k);
+            f[k] = divk(rk, (k & 1) ? 1.0 : -1.0, k);
             rk = rk * r;
         }
     } else {
@@ -85,30 +85,79 @@ template <class T, int K> __device__ __forceinline__ void outer_coefs(uint32_t o
         const T r = recip(x0);
         f[0] = f0;
 #pragma unroll
-        for (int k = 1; k <= K + 1; ++k) f[k] = f[k - 1] * r * ((a - (k - 1)) / k);
+        for (int k = 1; k <= K + 1; ++k) f[k] = divk(f[k - 1] * r, a - (k - 1), k);
     }
 }
 
-template <class T, int K, int MAXD> struct ErrInterp {
+// Operand-stack storage of the error-bounded interpreter (slots below the top of stack):
+//   LdsStack   per wave in LDS, [slot][coef][lane] (one wave = one candidate, or one candidate
+//              per lane with MAXD = 2)
+//   PrivStack  per lane in private memory (the compiler places it in scratch: dynamic slot
+//              index), for the rare list-driven point kernels of deep / complex / dd programs
+template <class T, int NC> struct LdsStack {
+    T* vs;
+    double* es;
+    int lane;
+    __device__ __forceinline__ void store(int slot, const T* t, const double* e) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            vs[(slot * NC + c) * 64 + lane] = t[c];
+            es[(slot * NC + c) * 64 + lane] = e[c];
+        }
+    }
+    __device__ __forceinline__ void load(int slot, T* t, double* e) const {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            t[c] = vs[(slot * NC + c) * 64 + lane];
+            e[c] = es[(slot * NC + c) * 64 + lane];
+        }
+    }
+};
+template <class T, int NC, int SLOTS> struct PrivStack {
+    T v[SLOTS][NC];
+    double e[SLOTS][NC];
+    __device__ __forceinline__ void store(int slot, const T* t, const double* ee) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            v[slot][c] = t[c];
+            e[slot][c] = ee[c];
+        }
+    }
+    __device__ __forceinline__ void load(int slot, T* t, double* ee) const {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            t[c] = v[slot][c];
+            ee[c] = e[slot][c];
+        }
+    }
+};
+
+// Immediate of an opcode as the coordinate type V: the f64 word pair, plus the double-double
+// low part when the opcode carries PDEVAL_IMM_DD and V = dd.
+template <class V, bool VEC> __device__ __forceinline__ V read_imm(const int32_t* p, uint32_t w) {
+    double hi, lo = 0.0;
+    if constexpr (VEC) {
+        hi = __hiloint2double(p[1], p[0]);
+        if constexpr (!std::is_same<V, double>::value)
+            if (w & PDEVAL_IMM_DD) lo = __hiloint2double(p[3], p[2]);
+    } else {
+        hi = rd_imm(p);
+        if constexpr (!std::is_same<V, double>::value)
+            if (w & PDEVAL_IMM_DD) lo = rd_imm(p + 2);
+    }
+    if constexpr (std::is_same<V, double>::value) {
+        (void)w;
+        return hi;
+    } else {
+        return V{hi, lo};
+    }
+}
+
+template <class T, int K, int MAXD, class V = double> struct ErrInterp {
     using O = JetOps<T, K>;
     using J = typename O::J;
     using E = EJ<K>;
     static constexpr int NC = nc(K);
-
-    static __device__ __forceinline__ void st(T* vs, double* es, int slot, int lane, const J& t, const double* e) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            vs[(slot * NC + c) * 64 + lane] = t.c[c];
-            es[(slot * NC + c) * 64 + lane] = e[c];
-        }
-    }
-    static __device__ __forceinline__ void ld(const T* vs, const double* es, int slot, int lane, J& t, double* e) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            t.c[c] = vs[(slot * NC + c) * 64 + lane];
-            e[c] = es[(slot * NC + c) * 64 + lane];
-        }
-    }
 
     // binary op t = a (op) t with error bounds (a = lhs with bound el), op in ADD..RDIV
     static __device__ __forceinline__ void binop_e(uint32_t op, const J& lhs, const double* el, J& acc, double* ea) {
@@ -151,11 +200,14 @@ template <class T, int K, int MAXD> struct ErrInterp {
     }
 
     // value + error bound of program words [pc, end) at (x, y)
-    // VEC: the program is per lane (pass 0, one candidate per lane): vector loads; otherwise it
-    // is wave-uniform and read through the scalar cache
-    template <bool VEC = false>
-    static __device__ int run(const int32_t* ops, int pc, int end, double x, double y, J& acc,
-                              double* ea, T* vs, double* es, int lane) {
+    // VEC: the program is per lane (one candidate per lane): vector loads; otherwise it is
+    // wave-uniform and read through the scalar cache.  STK: LdsStack / PrivStack.
+    // cerr: relative rounding error of the coordinates in noise units (0: exact grid points;
+    // the reference points 4/5, 6/7, 1/3 ... are not doubles, and near a pole of the candidate
+    // their rounding is amplified like any other error)
+    template <bool VEC, class STK>
+    static __device__ int run_s(const int32_t* ops, int pc, int end, V x, V y, J& acc, double* ea, STK& stk,
+                                double cerr = 0.0) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
         for (;;) {
@@ -163,28 +215,31 @@ template <class T, int K, int MAXD> struct ErrInterp {
             if constexpr (VEC) w = (uint32_t)ops[pc];
             else w = rd_word(ops + pc);
             const uint32_t op = w & 0xffu;
+            V immv = vzero<V>();
             double imm = 0.0;
             int npc = pc + 1;
             if (op_has_imm(op)) {
-                if (pc + 3 > end) return RUN_BAD;
-                if constexpr (VEC) imm = __hiloint2double(ops[pc + 2], ops[pc + 1]);
-                else imm = rd_imm(ops + pc + 1);
-                npc = pc + 3;
+                npc = pc + ((w & PDEVAL_IMM_DD) ? 5 : 3);
+                if (npc > end) return RUN_BAD;
+                immv = read_imm<V, VEC>(ops + pc + 1, w);
+                imm = hi_of(immv);
             }
             double A[NC], B[NC], R[NC];
             switch (op) {
                 case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I: {
-                    if (d > 0 && d < MAXD) st(vs, es, d - 1, lane, acc, ea);
+                    if (d > 0 && d < MAXD) stk.store(d - 1, acc.c, ea);
                     if (op == PDOP_PUSH_X) O::set_var(acc, x, 0);
                     else if (op == PDOP_PUSH_Y) O::set_var(acc, y, 1);
-                    else if (op == PDOP_PUSH_C) O::set_const(acc, from_real<T>(imm));
+                    else if (op == PDOP_PUSH_C) O::set_const(acc, cvt<T>(immv));
                     else {
-                        if constexpr (Real<T>::cplx_pass) O::set_const(acc, cplx{0.0, 1.0});
+                        if constexpr (Real<T>::cplx_pass) O::set_const(acc, imag_unit<T>());
                         else return RUN_UNSUPPORTED;
                     }
 #pragma unroll
                     for (int i = 0; i < NC; ++i) ea[i] = 0.0;
                     if (op == PDOP_PUSH_C) ea[0] = fabs(imm);
+                    else if (op == PDOP_PUSH_X) ea[0] = vabs(x) * cerr;
+                    else if (op == PDOP_PUSH_Y) ea[0] = vabs(y) * cerr;
                     ++d;
                     break;
                 }
@@ -193,18 +248,18 @@ template <class T, int K, int MAXD> struct ErrInterp {
                     if (d >= 2 && d <= MAXD) {
                         J lhs;
                         double el[NC];
-                        ld(vs, es, d - 2, lane, lhs, el);
+                        stk.load(d - 2, lhs.c, el);
                         binop_e(op, lhs, el, acc, ea);
                     }
                     --d;
                     break;
                 }
                 case PDOP_ADDC:
-                    acc.c[0] = acc.c[0] + from_real<T>(imm);
+                    acc.c[0] = acc.c[0] + cvt<T>(immv);
                     ea[0] += fabs(imm) + mag(acc.c[0]);
                     break;
                 case PDOP_MULC:
-                    O::scale(acc, from_real<T>(imm));
+                    O::scale(acc, cvt<T>(immv));
 #pragma unroll
                     for (int i = 0; i < NC; ++i) ea[i] = ea[i] * fabs(imm) + mag(acc.c[i]);
                     break;
@@ -212,7 +267,7 @@ template <class T, int K, int MAXD> struct ErrInterp {
                     E::absv(acc.c, B);
 #pragma unroll
                     for (int i = 0; i < NC; ++i) A[i] = ea[i];
-                    O::rdivc(acc, from_real<T>(imm));
+                    O::rdivc(acc, cvt<T>(immv));
                     E::absv(acc.c, R);
                     E::mul(R, A, A);
                     A[0] += fabs(imm);
@@ -225,7 +280,8 @@ template <class T, int K, int MAXD> struct ErrInterp {
                 case PDOP_RDIV_P: {
                     // p = v**n as a (value, bound) operand of the generic binary ops; E_p = n |p|
                     const int n = (int)((w >> 8) & 0xffu);
-                    double pk[K + 1], ep[NC];
+                    V pk[K + 1];
+                    double ep[NC];
                     J p;
                     if ((w >> 16) & 1) {
                         O::pcoefs(y, n, pk);
@@ -235,9 +291,9 @@ template <class T, int K, int MAXD> struct ErrInterp {
                         O::template set_p<0>(p, pk);
                     }
 #pragma unroll
-                    for (int i = 0; i < NC; ++i) ep[i] = n * mag(p.c[i]);
+                    for (int i = 0; i < NC; ++i) ep[i] = n * mag(p.c[i]) * (1.0 + cerr);
                     if (op == PDOP_PUSH_P) {
-                        if (d > 0 && d < MAXD) st(vs, es, d - 1, lane, acc, ea);
+                        if (d > 0 && d < MAXD) stk.store(d - 1, acc.c, ea);
                         acc = p;
 #pragma unroll
                         for (int i = 0; i < NC; ++i) ea[i] = ep[i];
@@ -256,42 +312,49 @@ template <class T, int K, int MAXD> struct ErrInterp {
                 case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: {
                     const bool isx = (op == PDOP_ADD_X || op == PDOP_SUB_X);
                     const double sg = (op == PDOP_ADD_X || op == PDOP_ADD_Y) ? 1.0 : -1.0;
-                    acc.c[0] = acc.c[0] + from_real<T>(sg * (isx ? x : y));
+                    acc.c[0] = acc.c[0] + cvt<T>((isx ? x : y) * sg);
                     const int idx = isx ? ji(1, 0) : ji(0, 1);
                     acc.c[idx] = acc.c[idx] + from_real<T>(sg);
-                    ea[0] += mag(acc.c[0]);
+                    ea[0] += mag(acc.c[0]) + vabs(isx ? x : y) * cerr;
                     break;
                 }
                 case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: {
                     const int axis = (op == PDOP_MUL_X || op == PDOP_DIV_X) ? 0 : 1;
-                    const double v = axis == 0 ? x : y;
+                    const V v = axis == 0 ? x : y;
                     if (op == PDOP_MUL_X || op == PDOP_MUL_Y) {
+                        // the coordinate's own rounding: t * dv, |t| |v| cerr per coefficient
+                        double cv[NC];
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) cv[i] = mag(acc.c[i]) * vabs(v) * cerr;
                         O::mul_var(acc, v, axis);
                         // E (*) (|v| + d_axis), in place in decreasing degree
 #pragma unroll
-                        for (int dd = K; dd >= 0; --dd)
+                        for (int dd_ = K; dd_ >= 0; --dd_)
 #pragma unroll
-                            for (int j = 0; j <= dd; ++j) {
-                                const int i = dd - j;
-                                double s = ea[ji(i, j)] * fabs(v);
+                            for (int j = 0; j <= dd_; ++j) {
+                                const int i = dd_ - j;
+                                double s = ea[ji(i, j)] * vabs(v);
                                 if (axis == 0 && i > 0) s += ea[ji(i - 1, j)];
                                 if (axis == 1 && j > 0) s += ea[ji(i, j - 1)];
-                                ea[ji(i, j)] = s;
+                                ea[ji(i, j)] = s + cv[ji(i, j)];
                             }
                     } else {
                         O::div_var(acc, v, axis);
                         // absdiv(E, |v| + d_axis), in place in increasing degree
-                        const double inv = 1.0 / fabs(v);
+                        const double inv = 1.0 / vabs(v);
 #pragma unroll
-                        for (int dd = 0; dd <= K; ++dd)
+                        for (int dd_ = 0; dd_ <= K; ++dd_)
 #pragma unroll
-                            for (int j = 0; j <= dd; ++j) {
-                                const int i = dd - j;
+                            for (int j = 0; j <= dd_; ++j) {
+                                const int i = dd_ - j;
                                 double s = ea[ji(i, j)];
                                 if (axis == 0 && i > 0) s += ea[ji(i - 1, j)];
                                 if (axis == 1 && j > 0) s += ea[ji(i, j - 1)];
                                 ea[ji(i, j)] = s * inv;
                             }
+                        // the coordinate's rounding: coefficient k of 1/(v + d) moves by (k+1) dv/v
+#pragma unroll
+                        for (int i = 0; i < NC; ++i) ea[i] += mag(acc.c[i]) * (cerr * (K + 1));
                     }
                     E::add_abs(acc.c, ea);
                     break;
@@ -299,12 +362,11 @@ template <class T, int K, int MAXD> struct ErrInterp {
                 case PDOP_POWN: {
                     // b^n as n-1 products by b: E' = P (*) (E_b + |b|) + E (*) |b|, P >= |b^k|
                     const int n = (int)((w >> 8) & 0xffu);
-                    double P[NC], eb[NC];
+                    double P[NC];
                     E::absv(acc.c, B);
 #pragma unroll
                     for (int i = 0; i < NC; ++i) {
                         P[i] = B[i];
-                        eb[i] = ea[i];
                         R[i] = ea[i] + B[i];
                     }
                     for (int k = 1; k < n; ++k) {
@@ -314,7 +376,6 @@ template <class T, int K, int MAXD> struct ErrInterp {
                         for (int i = 0; i < NC; ++i) ea[i] += A[i];
                         E::mul(P, B, P);
                     }
-                    (void)eb;
                     O::pown(acc, n);
                     break;
                 }
@@ -346,6 +407,14 @@ template <class T, int K, int MAXD> struct ErrInterp {
             pc = npc;
         }
         return d == 1 ? RUN_OK : RUN_BAD;
+    }
+
+    // the LDS-stack form used by the tier-2 and diagnostic kernels
+    template <bool VEC = false>
+    static __device__ int run(const int32_t* ops, int pc, int end, V x, V y, J& acc, double* ea, T* vs,
+                              double* es, int lane) {
+        LdsStack<T, NC> stk{vs, es, lane};
+        return run_s<VEC>(ops, pc, end, x, y, acc, ea, stk);
     }
 };
 
@@ -534,109 +603,3 @@ __global__ __launch_bounds__(64, 1) void eval_points_kernel(const int32_t* prog,
 }
 }  // namespace pd
 
-namespace pd {
-// Pass 0 (the point stage): one candidate per LANE.  Every real candidate of stack <= 2 is
-// evaluated at the reference point(s) with the error-bounded interpreter (tier 1 and tier 2
-// in one go, as tier2_kernel's point stage), so the point verdict -- the reference's first
-// stage, validator.py:349-402 / kerr :163-192 -- is final here:
-//   pstate[cand] = P0_PASS | P0_REJECT | P0_CPLX (appended to the complex list) | 0 (not taken:
-//   deeper stack, malformed, ...; pass 1 then runs its own point stage), + P0_GRAD if a
-// reference point has a non-zero gradient.  The lanes of a wave interpret different programs
-// (divergent dispatch), which is still ~64x the lane use of one wave per candidate.
-
-template <int PROB>
-__global__ __launch_bounds__(256, 1) void point_kernel(KernelArgs a) {
-    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
-    constexpr int NC = nc(K);
-    constexpr int MAXD = 2;
-    using EI = ErrInterp<double, K, MAXD>;
-    using J = typename EI::J;
-    const int lane = threadIdx.x & 63;
-    const int wib = threadIdx.x >> 6;
-#ifndef PD_HOST_SIM
-    extern __shared__ __align__(16) unsigned char pd_lds[];
-#else
-    static unsigned char pd_lds[1];
-#endif
-    double* vs = reinterpret_cast<double*>(pd_lds) + (size_t)wib * 2 * (MAXD - 1) * NC * 64;
-    double* es = vs + (size_t)(MAXD - 1) * NC * 64;
-    const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cand >= a.n) return;
-    const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
-    uint8_t ps = P0_NONE;
-    const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24);
-    if (in_bounds) {
-        const int32_t* prog = a.ops + beg;
-        const uint32_t hdr = (uint32_t)prog[0];
-        const int depth = (int)((hdr >> 8) & 0xffu);
-        if ((hdr & 0xffu) == 0u && depth <= MAXD) {
-            if (hdr & PDEVAL_FLAG_COMPLEX) {
-                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-                    if (a.cplx_list) {
-                        list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
-                        ps = P0_CPLX;
-                    }
-                } else {
-                    ps = P0_REJECT;          // Kerr: non-real at a test point (kerr validator.py:179-180)
-                }
-            } else {
-                double qr = 0.0;
-                bool nonfinite = false, reject = false, grad = false, prog_err = false;
-                for (int p = 0; p < a.n_ref; ++p) {
-                    const double x = p == 0 ? a.ref_x[0] : (p == 1 ? a.ref_x[1] : (p == 2 ? a.ref_x[2] : a.ref_x[3]));
-                    const double y = p == 0 ? a.ref_y[0] : (p == 1 ? a.ref_y[1] : (p == 2 ? a.ref_y[2] : a.ref_y[3]));
-                    J u;
-                    double e[NC];
-                    const int rc = EI::template run<true>(prog, 1, (int)(end - beg), x, y, u, e, vs, es, lane);
-                    if (rc != RUN_OK) { prog_err = true; break; }
-                    const double* kc = a.kc ? a.kc + 4 * p : nullptr;
-                    PointResult r;
-                    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);
-                    else r = kerr_epilogue<double>(u.c, kc);
-                    if (p == 0 && a.out.fingerprint) a.out.fingerprint[cand * PDEVAL_FP_N] = u.c[0];
-                    if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = r.res_re;
-                    if (!r.finite) { nonfinite = true; continue; }
-                    if (!r.grad_zero) grad = true;
-                    double v;
-                    bool fails;
-                    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-                        v = scaled(r.res_abs, r.scale);
-                        fails = !(v <= a.prm.tau_point);
-                    } else {
-                        v = r.res_abs;
-                        fails = !(v < a.prm.kerr_abs_tol);
-                    }
-                    qr = fmax(qr, v);
-                    if (fails && r.res_abs > a.prm.noise_kappa * residual_noise<PROB, double>(u.c, e, x, kc, r.scale))
-                        reject = true;
-                }
-                if (!prog_err) {
-                    if (a.out.q_ref) a.out.q_ref[cand] = qr;
-                    if (nonfinite) {
-                        if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-                            // not real at p*: the complex pass decides (validator.py:363-402)
-                            if (a.cplx_list) {
-                                list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
-                                ps = P0_CPLX;
-                            }
-                        } else {
-                            ps = P0_REJECT;  // Kerr: non-real / NaN at a test point
-                        }
-                    } else {
-                        ps = reject ? P0_REJECT : P0_PASS;
-                    }
-                    if (grad) ps |= P0_GRAD;
-                }
-            }
-        }
-    }
-    a.pstate[cand] = ps;
-    if ((ps & 3) == P0_REJECT && !a.prm.full_grid) {
-        // the reference's control flow: a point-stage reject is final
-        if (a.out.status) a.out.status[cand] = PDEVAL_CLS_REJECT_POINT;
-        if (a.out.q_grid) a.out.q_grid[cand] = 0.0;
-        if (a.out.n_bad) a.out.n_bad[cand] = 0;
-        if (a.out.n_nonfinite) a.out.n_nonfinite[cand] = 0;
-    }
-}
-}  // namespace pd

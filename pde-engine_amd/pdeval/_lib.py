@@ -23,18 +23,19 @@ EXPORTS = (
     'pdeval_n_points', 'pdeval_default_params', 'pdeval_validate_batch',
     'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
     'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts', 'pdeval_eval_points',
-    'pdeval_compile_batch', 'pdeval_canonical',
+    'pdeval_compile_batch', 'pdeval_canonical', 'pdeval_point_eval', 'pdeval_point_states',
 )
 LIST_NAMES = ('defer_stack3', 'complex', 'defer_stack8', 'tier2', 'tier2_stack3', 'tier2_complex',
-              'complex_stack8', 'tier2_stack8')
-N_PASSES = 10
+              'complex_stack8', 'tier2_stack8', 'point_deep', 'point_dd', 'point_dd_complex')
+N_PASSES = 12
 
 
 class Params(C.Structure):
     _fields_ = [('tau_point', C.c_double), ('tau_grid', C.c_double),
                 ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32),
                 ('strict_symbolic', C.c_int32), ('reserved', C.c_int32),
-                ('noise_kappa', C.c_double)]
+                ('noise_kappa', C.c_double), ('point_abs_tol', C.c_double),
+                ('res_rel_acc', C.c_double)]
 
 
 class Outputs(C.Structure):
@@ -80,6 +81,8 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_eval_points.argtypes = [vp, vp, i64, vp, vp, C.c_int, C.c_int, vp, vp]
     lib.pdeval_compile_batch.argtypes = [C.c_int, vp, vp, i64, vp, i64, vp, vp, vp]
     lib.pdeval_canonical.argtypes = [C.c_int, C.c_char_p, i64, C.c_char_p, i64]
+    lib.pdeval_point_eval.argtypes = [vp, vp, i64, C.c_int, vp, vp]
+    lib.pdeval_point_states.argtypes = [vp, vp, i64]
     for name in EXPORTS:
         getattr(lib, name)   # every symbol of the header must resolve
     if path is None:
@@ -181,6 +184,22 @@ class Context:
         _check(self.h, self.lib.pdeval_eval_points(self.h, _ptr(w), w.size, _ptr(x), _ptr(y), len(x),
                                                    int(tier2), _ptr(out), _ptr(jt)))
         return (out, jt) if jets else out
+
+    def point_eval(self, words, tier: int):
+        """(n_ref, 6) array {Re res, Im res, |res|, S, noise, finite} of one program at the
+        reference points in precision tier 0 fp64 / 1 complex / 2 double-double / 3 complex dd,
+        and the tier's point-stage decision (PDEVAL_PS_* bits)."""
+        w = np.ascontiguousarray(words, dtype=np.int32)
+        out = np.zeros((self.n_ref, 6))
+        st = np.zeros(1, dtype=np.uint8)
+        _check(self.h, self.lib.pdeval_point_eval(self.h, _ptr(w), w.size, tier, _ptr(out), _ptr(st)))
+        return out, int(st[0])
+
+    def point_states(self, n: int) -> np.ndarray:
+        """Point-stage state (PDEVAL_PS_* bits) of every candidate of the most recent call."""
+        out = np.zeros(n, dtype=np.uint8)
+        _check(self.h, self.lib.pdeval_point_states(self.h, _ptr(out), n))
+        return out
 
     def pass_counts(self):
         """{work list: entries} of the most recent call (synchronizes)."""

@@ -13,7 +13,9 @@ We take the same tree and compile it for the kernel:
 * children are emitted in Sethi-Ullman order (the operand needing more stack goes first, with
   reversed opcodes ``RSUB``/``RDIV`` for non-commutative ops) which keeps the operand stack --
   held in VGPRs on the device -- as shallow as the tree allows;
-* constants are folded to IEEE doubles (rationals correctly rounded from the exact p/q).
+* constants are folded to IEEE doubles (rationals correctly rounded from the exact p/q); a
+  constant that is not exactly a double (1/3, 1/10, E) also carries the low part of its
+  double-double value (opcode flag IMM_DD) for the point stage's double-double tier.
 
 The output is a list of int32 words: a header (opcode 0, stack depth in bits 8-15, flags in
 bits 16-31), then the postfix body; opcodes with an immediate are followed by its two words.
@@ -27,8 +29,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import sympy as sp
 
-from .opcodes import (PDOP, HAS_IMM, P_OPS, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD, FLAG_RATIONAL,
-                      FLAG_NONSMOOTH2D)
+from .opcodes import (PDOP, HAS_IMM, IMM_DD, P_OPS, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD,
+                      FLAG_RATIONAL, FLAG_NONSMOOTH2D, op_len)
 
 
 class Unsupported(Exception):
@@ -36,9 +38,16 @@ class Unsupported(Exception):
 
 
 # --------------------------------------------------------------------------- IR
-# nodes: ('x',) ('y',) ('i',) ('c', float)
+# nodes: ('x',) ('y',) ('i',) ('c', value, exact, rational)
 #        (op, child) for op in neg sqrt exp log abs;  ('pown', child, n);  ('pow', child, alpha)
 #        (op, a, b) for op in add sub mul div
+# A constant keeps its exact value (a Fraction; E and pi to 60 digits) beside the rounded
+# double: the double-double point tier needs the low part (_Emit.op), and rational marks the
+# constants _det_kind treats as rational.
+E_EXACT = Fraction('2.71828182845904523536028747135266249775724709369995957496697')
+PI_EXACT = Fraction('3.14159265358979323846264338327950288419716939937510582097494')
+
+
 def _is_pvar(n) -> bool:
     """A coordinate power x**n / y**n (2 <= n <= 16): fused into PUSH_P / ADD_P / ... ."""
     return n[0] == 'pown' and n[1][0] in ('x', 'y') and 2 <= n[2] <= 16
@@ -48,10 +57,36 @@ def _is_leaf(n) -> bool:
     return n[0] in ('x', 'y', 'c') or _is_pvar(n)
 
 
-def _const(v, rational: bool = True) -> tuple:
-    # ('c', value) for a rational constant, ('c', value, False) for an irrational one (E, pi,
-    # a Float); only _det_kind looks at the third field
-    return ('c', float(v)) if rational else ('c', float(v), False)
+def _cfrac(ex: Optional[Fraction], rational: bool = True) -> tuple:
+    """Constant node from its exact value (None: NaN)."""
+    if ex is None:
+        return ('c', float('nan'), None, rational)
+    return ('c', float(ex), ex, rational)
+
+
+def _cnum(e: sp.Basic) -> tuple:
+    """Constant node of a SymPy number (Integer, Rational, Float)."""
+    if e.is_Rational:
+        return _cfrac(Fraction(int(e.p), int(e.q)))
+    v = float(e)
+    return ('c', v, Fraction(v) if math.isfinite(v) else None, False)
+
+
+def _cneg(n) -> tuple:
+    return ('c', -n[1], None if n[2] is None else -n[2], n[3])
+
+
+def _crecip(n) -> tuple:
+    if n[2] is None or n[2] == 0:
+        return ('c', 1.0 / n[1] if n[1] else float('inf'), None, n[3])
+    return ('c', float(1 / n[2]), 1 / n[2], n[3])
+
+
+def _clo(n) -> float:
+    """Low part of the constant's double-double value (0 if the double is exact)."""
+    if n[2] is None or not math.isfinite(n[1]):
+        return 0.0
+    return float(n[2] - Fraction(n[1]))
 
 
 def _num_to_float(e: sp.Basic) -> float:
@@ -79,20 +114,20 @@ class _Lower:
                 return ('y',)
             for s, v in self.consts.items():
                 if e == s or e.name == s.name:
-                    return _const(_num_to_float(sp.nsimplify(v)) if not isinstance(v, float) else v)
+                    return _cnum(sp.nsimplify(v) if not isinstance(v, float) else sp.Float(v))
             raise Unsupported(f'free symbol {e}')
         if e is sp.nan or e is sp.zoo or e is sp.oo or e is sp.S.NegativeInfinity:
-            return _const(float('nan'))     # the driver's pre-validate filter drops these
+            return _cfrac(None)     # the driver's pre-validate filter drops these
         if e.is_Number:
             if not e.is_Rational:
                 self.irrational_const = True
-            return _const(_num_to_float(e), bool(e.is_Rational))
+            return _cnum(e)
         if e is sp.E:
             self.irrational_const = True
-            return _const(math.e, False)
+            return _cfrac(E_EXACT, False)
         if e is sp.pi:
             self.irrational_const = True
-            return _const(math.pi, False)
+            return _cfrac(PI_EXACT, False)
         if e is sp.I:
             self.uses_i = True
             return ('i',)
@@ -111,13 +146,14 @@ class _Lower:
         raise Unsupported(f'{type(e).__name__}')
 
     def add(self, e: sp.Add):
-        const = 0.0
+        const = Fraction(0)
         have_const = False
         const_rational = True
         terms: List[Tuple[int, tuple]] = []
         for t in e.args:
             if t.is_Number and t.is_real:
-                const += _num_to_float(t)
+                c = _cnum(t)
+                const = None if const is None or c[2] is None else const + c[2]
                 have_const = True
                 const_rational = const_rational and bool(t.is_Rational)
                 continue
@@ -128,7 +164,7 @@ class _Lower:
                 sign = -1
             terms.append((sign, self.node(t)))
         if not terms:
-            return _const(const, const_rational)
+            return _cfrac(const, const_rational)
         # positive terms first (so no leading negation is needed), heavy operands first
         terms.sort(key=lambda st: (st[0] < 0, -_need(st[1])))
         sign, acc = terms[0]
@@ -136,18 +172,19 @@ class _Lower:
             acc = ('neg', acc)
         for sign, t in terms[1:]:
             acc = ('add' if sign > 0 else 'sub', acc, t)
-        if have_const and const != 0.0:
-            acc = ('add', acc, _const(const, const_rational))
+        if have_const and const != 0:
+            acc = ('add', acc, _cfrac(const, const_rational))
         return acc
 
     def mul(self, e: sp.Mul):
-        coef = 1.0
+        coef = Fraction(1)
         coef_rational = True
         num: List[tuple] = []
         den: List[tuple] = []
         for f in e.args:
             if f.is_Number and f.is_real:
-                coef *= _num_to_float(f)
+                c = _cnum(f)
+                coef = None if coef is None or c[2] is None else coef * c[2]
                 coef_rational = coef_rational and bool(f.is_Rational)
                 continue
             if f.is_Pow and f.exp.is_Integer and f.exp < 0:
@@ -168,14 +205,14 @@ class _Lower:
             acc = product(num)
             if den:
                 acc = ('div', acc, product(den))
-            if coef == -1.0:
+            if coef == -1:
                 acc = ('neg', acc)
-            elif coef != 1.0:
-                acc = ('mul', acc, _const(coef, coef_rational))
+            elif coef != 1:
+                acc = ('mul', acc, _cfrac(coef, coef_rational))
             return acc
         if den:
-            return ('div', _const(coef, coef_rational), product(den))
-        return _const(coef, coef_rational)
+            return ('div', _cfrac(coef, coef_rational), product(den))
+        return _cfrac(coef, coef_rational)
 
     def _pown(self, b, n: int):
         if n == 1:
@@ -188,11 +225,11 @@ class _Lower:
         if ex.is_Integer:
             n = int(ex)
             if n == 0:
-                return _const(1.0)
+                return _cfrac(Fraction(1))
             b = self.node(base)
             if n > 0:
                 return self._pown(b, n)
-            return ('div', _const(1.0), self._pown(b, -n))
+            return ('div', _cfrac(Fraction(1)), self._pown(b, -n))
         if ex.is_Rational:
             b = self.node(base)
             if ex == sp.Rational(1, 2):
@@ -229,13 +266,16 @@ class _Emit:
         self.d = 0
         self.dmax = 0
 
-    def op(self, name: str, imm: Optional[float] = None, arg: int = 0):
+    def op(self, name: str, imm: Optional[float] = None, arg: int = 0, imm_lo: float = 0.0):
         code = PDOP[name]
+        if code in HAS_IMM and imm_lo != 0.0:
+            arg |= IMM_DD >> 8
         self.w.append(code | (arg << 8))
         if code in HAS_IMM:
-            lo, hi = struct.unpack('<II', struct.pack('<d', float(imm)))
-            self.w.append(_s32(lo))
-            self.w.append(_s32(hi))
+            for v in ((imm, imm_lo) if imm_lo != 0.0 else (imm,)):
+                lo, hi = struct.unpack('<II', struct.pack('<d', float(v)))
+                self.w.append(_s32(lo))
+                self.w.append(_s32(hi))
         if name.startswith('PUSH'):
             self.d += 1
             self.dmax = max(self.dmax, self.d)
@@ -256,7 +296,7 @@ class _Emit:
         elif n[0] == 'i':
             self.op('PUSH_I')
         else:
-            self.op('PUSH_C', n[1])
+            self.op('PUSH_C', n[1], imm_lo=_clo(n))
 
     def fused(self, k: str, leaf) -> bool:
         """top = top (k) leaf as one opcode, if one exists."""
@@ -268,16 +308,17 @@ class _Emit:
         if t == 'c':
             c = leaf[1]
             if k == 'add':
-                self.op('ADDC', c)
+                self.op('ADDC', c, imm_lo=_clo(leaf))
             elif k == 'sub':
-                self.op('ADDC', -c)
+                self.op('ADDC', -c, imm_lo=-_clo(leaf))
             elif k == 'mul':
                 if c == -1.0:
                     self.op('NEG')
                 else:
-                    self.op('MULC', c)
+                    self.op('MULC', c, imm_lo=_clo(leaf))
             elif k == 'div':
-                self.op('MULC', 1.0 / c)
+                r = _crecip(leaf)
+                self.op('MULC', r[1], imm_lo=_clo(r))
             return True
         if t in ('x', 'y'):
             ax = 'X' if t == 'x' else 'Y'
@@ -318,7 +359,7 @@ class _Emit:
             return
         if k == 'div' and a[0] == 'c':          # c / b
             self.emit(b)
-            self.op('RDIVC', a[1])
+            self.op('RDIVC', a[1], imm_lo=_clo(a))
             return
         if k == 'div' and _is_pvar(a):          # v**n / b
             self.emit(b)
@@ -352,7 +393,7 @@ def _op_positions(body: Sequence[int]):
     i = 0
     while i < len(body):
         yield i
-        i += 3 if (body[i] & 0xff) in HAS_IMM else 1
+        i += op_len(body[i])
 
 
 # --------------------------------------------------------------------------- det rationality
@@ -378,7 +419,7 @@ def _det_kind(n):
     if k in ('x', 'y'):
         return 'R'
     if k == 'c':
-        return 'R' if len(n) == 2 else 'C'
+        return 'R' if n[3] else 'C'
     if k == 'i':
         return None
     if k in ('neg', 'abs'):
@@ -437,10 +478,10 @@ def det_rational(ir) -> bool:
             if b[0] == 'c' or _det_kind(b) == 'C':
                 n = a
                 continue
-        elif k == 'mul' and n[1][0] == 'c' and len(n[1]) == 2:
+        elif k == 'mul' and n[1][0] == 'c' and n[1][3]:
             n = n[2]
             continue
-        elif k in ('mul', 'div') and n[2][0] == 'c' and len(n[2]) == 2:
+        elif k in ('mul', 'div') and n[2][0] == 'c' and n[2][3]:
             n = n[1]
             continue
         break
@@ -488,14 +529,19 @@ def disasm(words: Sequence[int]) -> str:
     out = [f'HEADER depth={program_depth(words)} flags={words[0] >> 16:#x}']
     i = 1
     while i < len(words):
-        w = words[i] & 0xffffffff
+        w = int(words[i]) & 0xffffffff
         op = w & 0xff
         name = OP_NAME.get(op, f'?{op}')
         if op in HAS_IMM:
-            lo, hi = words[i + 1] & 0xffffffff, words[i + 2] & 0xffffffff
+            lo, hi = int(words[i + 1]) & 0xffffffff, int(words[i + 2]) & 0xffffffff
             v = struct.unpack('<d', struct.pack('<II', lo, hi))[0]
-            out.append(f'{name} {v!r}')
-            i += 3
+            if w & IMM_DD:
+                lo2, hi2 = int(words[i + 3]) & 0xffffffff, int(words[i + 4]) & 0xffffffff
+                v2 = struct.unpack('<d', struct.pack('<II', lo2, hi2))[0]
+                out.append(f'{name} {v!r} + {v2!r}')
+            else:
+                out.append(f'{name} {v!r}')
+            i += op_len(w)
         else:
             if op in P_OPS:
                 out.append(f"{name} {'xy'[(w >> 16) & 1]}^{(w >> 8) & 0xff}")

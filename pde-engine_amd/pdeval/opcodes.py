@@ -15,6 +15,15 @@ PDOP = dict(
 )
 OP_NAME = {v: k for k, v in PDOP.items()}
 HAS_IMM = {PDOP['PUSH_C'], PDOP['ADDC'], PDOP['MULC'], PDOP['RDIVC'], PDOP['POW']}
+# bit 8 of an immediate-carrying opcode word: a double-double low part (2 more words) follows
+IMM_DD = 1 << 8
+
+
+def op_len(word: int) -> int:
+    """Words taken by the opcode `word` and its immediate(s)."""
+    if (word & 0xff) in HAS_IMM:
+        return 5 if word & IMM_DD else 3
+    return 1
 # opcodes whose operand (bits 8-23) is a coordinate power v**n: n in bits 8-15, axis in bit 16
 P_OPS = {PDOP[k] for k in ('PUSH_P', 'ADD_P', 'SUB_P', 'MUL_P', 'DIV_P', 'RDIV_P')}
 

@@ -98,7 +98,10 @@ class KerrMagnetosphereValidator:
                     'max_scaled_lhs_on_grid': v.q_grid,
                     'params': {'M': str(self.M_value), 'a': str(self.a_value)},
                 }
-                if v.cls in (1, 2):
+                # the reference consults its cache only after the fast point check passed and
+                # writes False only when the exact-zero stage failed (:274-281, :308-315): a
+                # repeated point reject is re-checked (same reason), a grid reject is "(cached)"
+                if v.cls == 2:
                     self._residual_zero_cache[str(u)] = False
                 if ok and not defer_heavy_checks:
                     ok, reason = self._heavy_checks(u, check_regularity, enforce_anchor)

@@ -31,13 +31,14 @@ class _Params(C.Structure):
     _fields_ = [('tau_point', C.c_double), ('tau_grid', C.c_double),
                 ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32),
                 ('strict_symbolic', C.c_int32), ('reserved', C.c_int32),
-                ('noise_kappa', C.c_double)]
+                ('noise_kappa', C.c_double), ('point_abs_tol', C.c_double),
+                ('res_rel_acc', C.c_double)]
 
 
 def params(tau_point=1e-10, tau_grid=1e-7, kerr_abs_tol=1e-10, full_grid=1, max_bad=0,
-           strict_symbolic=1, noise_kappa=16.0):
+           strict_symbolic=1, noise_kappa=16.0, point_abs_tol=1e-20, res_rel_acc=1e-11):
     return _Params(tau_point, tau_grid, kerr_abs_tol, full_grid, max_bad, strict_symbolic, 0,
-                   noise_kappa)
+                   noise_kappa, point_abs_tol, res_rel_acc)
 
 
 def validate(problem_id, ops, offsets, prm=None, first=0, count=-1, n_ref=None):

@@ -41,10 +41,13 @@ def test_opcodes_match_header():
 
 def test_params_struct_layout():
     import ctypes as C
-    assert C.sizeof(_lib.Params) == 48
+    assert C.sizeof(_lib.Params) == 64
     assert C.sizeof(_lib.Outputs) == 64
     p = _lib.default_params(0)
     assert p.tau_point == 1e-10 and p.kerr_abs_tol == 1e-10 and p.full_grid == 1
+    assert p.point_abs_tol == 1e-20 and p.res_rel_acc == 1e-11 and p.noise_kappa == 16.0
+    assert int(re.search(r'PDEVAL_N_PASSES\s+(\d+)', HEADER).group(1)) == _lib.N_PASSES
+    assert int(re.search(r'PDEVAL_IMM_DD\s+\(1u << (\d+)\)', HEADER).group(1)) == OPC.IMM_DD.bit_length() - 1
 
 
 def test_program_depth_checks():

@@ -1,9 +1,13 @@
 """GPU parity: libpdeval.so on the MI355X vs the CPU oracle and vs the reference's verdicts.
 
 Bar (north star): accept/reject verdicts identical to the reference's on every fixture the
-reference decided; residuals at the reference point(s) within 1e-10 relative of the oracle's
-(absolute floor 1e-13 * S for residuals that are rounding noise of an exact zero).
+reference decided, reason classes identical (100 %), and residuals at the reference point(s)
+within 1e-10 relative of the exact values (tests/golden/exact/, SymPy exact arithmetic) and of
+the oracle's quad-precision point stage wherever the residual is non-zero.
 """
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -11,6 +15,7 @@ import golden_data as G
 import oracle_lib as O
 from pdeval import problem_defs as P
 from pdeval._lib import Context
+from pdeval.opcodes import FLAG_COMPLEX
 
 pytestmark = pytest.mark.gpu
 
@@ -18,21 +23,21 @@ REL_TOL = 1e-10
 EPS = 2.0 ** -52
 
 
-def check_residuals(dev, ora, strings, tau=1e-10):
-    """Residual at the reference point(s) of every point-stage reject (class REJECT_POINT):
-    the device value agrees with the oracle's to 1e-10 relative -- or, where the residual
-    itself is the result of cancellation, to the fp64 conditioning limit 64 eps / q (neither
-    side is exact there).  Every other candidate's residual is rounding noise of an exact
-    zero (q <= tau, or |res| within its noise bound: tier 2), which the equal classes already
-    assert."""
-    q = np.asarray(ora['q_ref'])
+def check_residuals(dev, ora, strings):
+    """Residual at the reference point(s) of every point-stage reject (class REJECT_POINT, so
+    the residual is non-zero): the device value (fp64 where its error bound makes it accurate
+    to 1e-11, else the double-double tier) agrees with the oracle's quad-precision value to
+    1e-10 relative, with no loosening.  (Force-free rejects at one point; a Kerr point reject
+    needs one of its three points >= 1e-10, so only those points are compared.)  Every other
+    residual is rounding noise of an exact zero, which the equal classes already assert."""
     d, o = dev['res_ref'], ora['res_ref']
-    for i in range(len(q)):
-        if ora['status'][i] != 1 or not (q[i] > tau) or not np.all(np.isfinite(o[i])):
-            continue
-        tol = max(REL_TOL, 64 * EPS / q[i]) if dev['res_ref'].shape[1] == 1 else REL_TOL
-        err = np.max(np.abs(d[i] - o[i]) / np.maximum(np.abs(o[i]), 1e-300))
-        assert err <= tol, (strings[i], d[i], o[i], err, tol)
+    for i in range(len(o)):
+        if ora['status'][i] != 1 or not np.all(np.isfinite(o[i])) or not np.all(np.isfinite(d[i])):
+            continue    # (a non-finite value is an exact pole: both reject, kerr validator.py:179-183)
+        pts = [0] if o.shape[1] == 1 else [k for k in range(o.shape[1]) if abs(o[i, k]) >= 1e-10]
+        for k in pts:
+            err = abs(d[i, k] - o[i, k]) / max(abs(o[i, k]), 1e-300)
+            assert err <= REL_TOL, (strings[i], k, d[i, k], o[i, k], err)
 
 
 @pytest.fixture(scope='module')
@@ -46,9 +51,16 @@ def _cmp_device_oracle(ctx, pd_, strings):
     ora = O.validate(pd_.problem_id, ops, off)
     assert np.array_equal(dev['status'], ora['status']), \
         [(s, int(a), int(b)) for s, a, b in zip(strings, dev['status'], ora['status']) if a != b][:10]
-    bad = np.flatnonzero(dev['n_bad'] != ora['n_bad'])
+    # n_bad decides the grid stage (tier 2 counts for grid rejects): equal wherever the grid
+    # decides; for a point reject (full_grid) it is only reported, a tier-1 count whose points
+    # near tau_grid depend on the evaluation order (device Horner vs oracle powers): 1 %
+    st = dev['status']
+    bad = np.flatnonzero((dev['n_bad'] != ora['n_bad']) & (st != 1))
     assert not bad.size, [(strings[i], int(dev['status'][i]), int(dev['n_bad'][i]), int(ora['n_bad'][i]))
                           for i in bad[:10]]
+    nb = np.abs(dev['n_bad'].astype(np.int64) - ora['n_bad'])
+    assert nb.max(initial=0) <= 41, [(strings[i], int(dev['n_bad'][i]), int(ora['n_bad'][i]))
+                                     for i in np.flatnonzero(nb > 41)[:10]]
     # n_nonfinite: points where an intermediate jet of the program overflows (exp(exp(..)))
     # depend on the evaluation order (device Horner vs oracle explicit powers); allow 1 % of
     # the grid there -- the classes above are exact
@@ -109,12 +121,102 @@ def test_plugin_api_reasons():
     us = [sp.sympify(r['expr'], locals=locs) for r in rows]
     got = prob.validator.validate_batch(us, check_regularity=False, fast_point_only=False)
     verdicts = sum(g[0] == r['ok'] for g, r in zip(got, rows))
-    cls = sum(g[1].split('≈')[0] == r['reason'].split('≈')[0] for g, r in zip(got, rows))
+    text = [(r['expr'], r['reason'], g[1]) for g, r in zip(got, rows) if g[1] != r['reason']]
     assert verdicts == len(rows)
-    assert cls >= 0.95 * len(rows), (cls, len(rows))
+    assert not text, text[:10]     # the reference's reason strings, digits included
     # the per-candidate contract of problems/__init__.py:52
     assert prob.validator.validate(us[0], check_regularity=False) == got[0]
     assert all(prob.validator.validate_known_solutions().values())
+
+
+def test_plugin_api_reasons_kerr():
+    """The Kerr plugin object through validate() / validate_batch() on the GPU: verdicts and
+    reason classes of every decided Kerr fixture (kerr validator.py:231-323)."""
+    from problems import load_problem
+    import sympy as sp
+    rows = G.decided(G.ref_rows(*G.KERR_REF, 'kerr_edge.jsonl'))
+    prob = load_problem('kerr_magnetosphere')
+    locs = {**prob.symbols, **prob.constants, **prob.unary_ops}
+    us = [sp.sympify(r['expr'], locals=locs) for r in rows]
+    got = prob.validator.validate_batch(us, check_regularity=False, fast_point_only=False,
+                                        lean_first=True, defer_heavy_checks=True, enforce_anchor=False)
+    bad = [(r['expr'], r['reason'][:60], g[1][:60]) for g, r in zip(got, rows)
+           if g[0] != r['ok'] or g[1].split('|')[0] != r['reason'].split('|')[0]]
+    assert not bad, bad[:10]
+    assert prob.validator.validate(us[0], check_regularity=False) == got[0]
+
+
+def test_ff_point_stage_exact_ground_truth(ff_ctx):
+    """The point stage decides like the reference (validator.py:371-397): on the 905
+    exact-determinant ground-truth candidates the device class is REJECT_POINT exactly when
+    |det(p*)| >= 1e-20, and res_ref is within 1e-10 relative of the exact |det(p*)|."""
+    pd_ = P.force_free()
+    rows = G.exact_rows()
+    ops, off, _ = P.compile_strings(pd_, [r['expr'] for r in rows])
+    dev = ff_ctx.validate(ops, off)
+    wrong = [(r['expr'], r['det_abs'][0], int(s)) for r, s in zip(rows, dev['status'])
+             if (s == 1) != (r['det_abs'][0] >= 1e-20)]
+    assert not wrong, wrong[:10]
+    err = [(rows[i]['expr'], abs(abs(dev['res_ref'][i, 0]) - rows[i]['det_abs'][0]) / rows[i]['det_abs'][0])
+           for i in range(len(rows)) if rows[i]['det_abs'][0] >= 1e-20]
+    assert max(e for _, e in err) <= REL_TOL, sorted(err, key=lambda t: -t[1])[:5]
+    counts = ff_ctx.pass_counts()
+    assert counts['point_dd'] > 0      # the double-double tier took part
+
+
+def test_ff_point_reject_hidden_in_fp64_noise(ff_ctx):
+    """exp(z/(-rho**2 + z**2)): exact det(p*) = -6.546893155e35, but S = 2.6e48 so fp64 cannot
+    tell it from 0.  The reference says 'Invalid (point check ≈ 6.55e+35)'
+    (tests/golden/ref/ff_d4_s500.jsonl); so must the device (double-double tier)."""
+    from pdeval.batch import reason_for
+    pd_ = P.force_free()
+    s = 'exp(z/(-rho**2 + z**2))'
+    ops, off, _ = P.compile_strings(pd_, [s])
+    dev = ff_ctx.validate(ops, off)
+    assert int(dev['status'][0]) == 1
+    ok, reason = reason_for(0, 1, dev['res_ref'][0], dev['q_ref'][0], dev['q_grid'][0], False)
+    assert reason == 'Invalid (point check ≈ 6.55e+35)', reason
+    assert abs(dev['res_ref'][0, 0] - (-6.546893154784001770635766939e35)) <= 1e-10 * 6.55e35
+
+
+def _exact_fixture(name):
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'exact', name)
+    if not os.path.exists(p):
+        pytest.skip(f'{name} not generated')
+    with open(p) as f:
+        return [json.loads(line) for line in f]
+
+
+@pytest.mark.parametrize('prob,name', [('force_free', 'ff_ref_exact.jsonl'),
+                                       ('force_free', 'ff_gt_exact.jsonl'),
+                                       ('kerr', 'kerr_ref_exact.jsonl')])
+def test_residuals_match_exact_values(ff_ctx, kerr_ctx, prob, name):
+    """Device res_ref against the exact residuals of every fixture (gen_exact_ref.py: sp.diff,
+    exact rational points, evalf(50)): within 1e-10 relative wherever |res| >= 1e-20
+    (force-free; complex residuals as their signed modulus) or >= 1e-10 (Kerr, the
+    reference's absolute threshold; below it the value is only compared with that threshold)."""
+    pd_ = P.get(prob)
+    ctx = ff_ctx if pd_.problem_id == 0 else kerr_ctx
+    rows = [r for r in _exact_fixture(name) if not r.get('timeout') and 'res' in r]
+    ops, off, _ = P.compile_strings(pd_, [r['expr'] for r in rows])
+    dev = ctx.validate(ops, off)
+    floor = 1e-20 if pd_.problem_id == 0 else 1e-10
+    bad, n = [], 0
+    for i, r in enumerate(rows):
+        if dev['status'][i] in (3, 5, 6):       # constant / unsupported: no point stage
+            continue
+        if pd_.problem_id == 1 and int(ops[off[i]]) & FLAG_COMPLEX:
+            continue                            # Kerr rejects non-real programs unevaluated
+        for k, (re_s, im_s) in enumerate(r['res']):
+            ex = complex(float(re_s), float(im_s))
+            if abs(ex) < floor or not np.isfinite(dev['res_ref'][i, k]):
+                continue
+            n += 1
+            err = abs(abs(dev['res_ref'][i, k]) - abs(ex)) / abs(ex)
+            if err > REL_TOL:
+                bad.append((r['expr'], k, dev['res_ref'][i, k], abs(ex), err))
+    assert n > 0
+    assert not bad, (len(bad), n, bad[:8])
 
 
 def test_ff_tier2_exact_ground_truth(ff_ctx):

@@ -16,7 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SO = os.path.join(HERE, 'hostsim', '_build', 'libsim.so')
 SRC = [os.path.join(ROOT, 'pde-engine_amd', 'csrc', f) for f in
-       ('pdeval_kernels.h', 'pdeval_tier2.h', 'jet.h')] + [os.path.join(HERE, 'hostsim', 'sim.cpp')]
+       ('pdeval_kernels.h', 'pdeval_tier2.h', 'pdeval_point.h', 'jet.h', 'dd.h')] + \
+      [os.path.join(HERE, 'hostsim', 'sim.cpp')]
 
 
 @pytest.fixture(scope='module')
@@ -29,6 +30,7 @@ def sim():
     lib = C.CDLL(SO)
     vp = C.c_void_p
     lib.sim_point.argtypes = [C.c_int, vp, C.c_int, C.c_double, C.c_double, C.c_int, vp, vp, vp]
+    lib.sim_point_tier.argtypes = [C.c_int, vp, C.c_int, C.c_int, C.c_int, vp]
     return lib
 
 
