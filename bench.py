@@ -12,9 +12,10 @@ determinant and its scaled zero test are applied and the verdict bitmap + per-ca
 outputs are written to HBM.  Inputs are resident in HBM before timing starts.
 
 Multi-GPU (torchrun, one process per GPU): the global batch (--n per rank) is cut into
-contiguous shards (pdeval.shard); every rank validates its own shard (weak scaling, no
-data-path collective); after timing, one RCCL all-gather of the verdict bitmaps assembles the
-global result on every rank.
+contiguous shards balanced by the programs' FLOP model (pdeval.shard); every rank validates its
+own shard (weak scaling, no data-path collective); after timing, one RCCL all-gather of the
+verdict bitmaps (pdeval_gather_bits, through the C ABI) assembles the global result on every
+rank, checked against torch.distributed's all-gather.
 """
 import argparse
 import ctypes as C
@@ -91,7 +92,7 @@ def main():
     import torch.distributed as dist
     from pdeval import _lib
     from pdeval.opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR, FP_N, FLAG_COMPLEX
-    from pdeval.shard import gather_verdicts, shard_ranges
+    from pdeval.shard import gather_verdicts, gather_verdicts_native, init_native_comm, shard_ranges
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -110,17 +111,17 @@ def main():
     rng = np.random.default_rng(0)
     tiled = np.tile(np.arange(nprog, dtype=np.int64), (total + nprog - 1) // nprog)[:total]
     rng.shuffle(tiled)
-    ranges = shard_ranges(total, world)
-    s0, s1 = ranges[rank]
-    idx = tiled[s0:s1]
-    n = len(idx)
-    ops, off = gather_programs(ops_all, off_all, idx)
 
-    # algorithmic work of the batch
+    # algorithmic work of the batch; it also balances the shards
     lib = _lib.load()
     flops_prog = np.array([lib.pdeval_program_flops(pid, ops_all[off_all[i]:].ctypes.data,
                                                     int(off_all[i + 1] - off_all[i]))
                            for i in range(nprog)])
+    ranges = shard_ranges(total, world, weights=flops_prog[tiled] if world > 1 else None)
+    s0, s1 = ranges[rank]
+    idx = tiled[s0:s1]
+    n = len(idx)
+    ops, off = gather_programs(ops_all, off_all, idx)
     ctx = _lib.Context(pid, device=local)
     npts, nref = ctx.n_points, ctx.n_ref
     flops_step = float(flops_prog[idx].sum()) * npts
@@ -176,9 +177,20 @@ def main():
 
     elapsed, kern_ms = timed(prm, a.steps, a.warmup)
 
-    # the one exchange step: all-gather of the verdict bitmaps over RCCL
+    # the one exchange step: all-gather of the verdict bitmaps over RCCL, through the C ABI
+    # (pdeval_gather_bits), checked against torch.distributed's all-gather
+    gather = None
     if world > 1:
         verdict_all = gather_verdicts(outs['verdict_bits'], ranges)
+        try:
+            init_native_comm(ctx, rank, world)
+            t0 = time.perf_counter()
+            native = gather_verdicts_native(ctx, outs['verdict_bits'], ranges)
+            gather = {'native_rccl_ms': round((time.perf_counter() - t0) * 1e3, 3),
+                      'native_equals_torch': bool(np.array_equal(native, verdict_all))}
+            verdict_all = native
+        except Exception as e:   # noqa: BLE001 -- reported; the torch gather result stands
+            gather = {'native_rccl_error': str(e)[:200]}
     else:
         verdict_all = np.unpackbits(outs['verdict_bits'].cpu().numpy(), bitorder='little')[:n].astype(bool)
     status = outs['status'].cpu().numpy()
@@ -241,6 +253,10 @@ def main():
             'status_hist': np.bincount(status, minlength=8).tolist(),
             'duplicates_consistent': consistent,
         }
+        if gather is not None:
+            res['gather'] = gather
+        if world > 1:
+            res['shard_balance'] = 'flops'
 
     if not a.no_extras and world == 1:
         # the reference's control flow: stop after the point stage for point-rejects (same

@@ -102,6 +102,8 @@ enum pdeval_opcode {
 };
 
 #define PDEVAL_MAX_STACK  8   /* deepest program stack any kernel variant accepts */
+#define PDEVAL_MAX_BATCH  ((int64_t)1 << 30)  /* largest n of one validate call (2^30 candidates;
+                                                 int32 work-list counters): PDEVAL_ERR_ARG beyond */
 
 /* Immediate-carrying opcode word (PUSH_C, ADDC, MULC, RDIVC): bit 8 set = a double-double
    low part follows the f64 immediate (2 more words, low word first).                    */
@@ -193,8 +195,9 @@ int pdeval_pass_times(pdeval_ctx* ctx, float* ms, int max_passes, const char** n
 /* Work-list sizes of the most recent call (synchronizes the device): [0] deferred to the
  * stack-3 pass, [1] complex passes, [2] deferred to the stack-8 pass, [3] tier-2 entries,
  * [4] tier-2 stack 3, [5] tier-2 complex, [6] complex stack 8, [7] tier-2 stack 8,
- * [8] deep point pass (real, stack 3..8), [9] double-double point tier (real),
- * [10] double-double point tier (complex).                                               */
+ * [8] deep point pass (real, stack 3..8), [9] double-double point tier (real, stack <= 2),
+ * [10] double-double point tier (complex), [11] double-double point tier (real, stack 3..8),
+ * [12] complex tier 2, stack 5..8.                                                        */
 int pdeval_pass_counts(pdeval_ctx* ctx, int64_t* counts, int max_counts);
 
 /* Diagnostics (force-free): one program at n_pts points (host arrays), tier-1 (tier2 = 0) or
@@ -220,6 +223,23 @@ int pdeval_eval_points(pdeval_ctx* ctx, const int32_t* prog, int64_t n_words, co
 int pdeval_point_eval(pdeval_ctx* ctx, const int32_t* prog, int64_t n_words, int tier, double* out,
                       uint8_t* state);
 int pdeval_point_states(pdeval_ctx* ctx, uint8_t* out, int64_t n);
+
+/* ---- multi-GPU: the one exchange step ----
+ * Candidate batches shard across GPUs with no data-path communication; the per-rank verdict
+ * bitmaps are then assembled with one RCCL all-gather over xGMI.  RCCL (librccl.so.1) is
+ * loaded on first use, so the library has no link-time dependency on it.
+ *   pdeval_comm_unique_id  on one rank: the 128-byte RCCL id, to be shared with every rank
+ *   pdeval_comm_init       on every rank (collective): world ranks, this one = rank, on the
+ *                          context's GPU
+ *   pdeval_gather_bits     d_local: this rank's nbytes (device), d_global: world * nbytes
+ *                          (device), rank r's bytes at offset r * nbytes; asynchronous on
+ *                          `stream` (NULL = the context's stream)
+ *   pdeval_comm_destroy    releases the communicator (also done by pdeval_destroy)        */
+#define PDEVAL_UNIQUE_ID_BYTES 128
+int pdeval_comm_unique_id(uint8_t* id);
+int pdeval_comm_init(pdeval_ctx* ctx, int world, int rank, const uint8_t* id);
+int pdeval_gather_bits(pdeval_ctx* ctx, const uint8_t* d_local, int64_t nbytes, uint8_t* d_global, void* stream);
+int pdeval_comm_destroy(pdeval_ctx* ctx);
 
 /* Host-side program analysis (no GPU): required stack depth, or < 0 if malformed.      */
 int pdeval_program_depth(const int32_t* ops, int64_t n_words);

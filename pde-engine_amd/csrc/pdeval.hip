@@ -5,7 +5,9 @@
 // passes (deep-stack programs, complex-valued candidates) and the launch sequence.  All device
 // allocation happens at create time or when a batch outgrows the scratch lists, never inside
 // an already-sized hot call, so pdeval_validate_device can be captured in a hipGraph.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -36,7 +38,9 @@ enum {
     L_PDEEP = 8,      // pass 0 -> deep point pass: real programs of stack 3..8
     L_DD = 9,         // double-double point tier, real
     L_DDC = 10,       // double-double point tier, complex
-    PD_N_LISTS = 11
+    L_DD8 = 11,       // double-double point tier, real, stack 3..8
+    L_ESC_C_DEEP = 12,  // complex tier 2, stack 5..8
+    PD_N_LISTS = 13
 };
 
 struct pdeval_ctx {
@@ -59,6 +63,7 @@ struct pdeval_ctx {
     int32_t* d_counts = nullptr;
     uint8_t* d_pstate = nullptr;    // point-stage state, capacity cap
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
+    double* d_noise = nullptr;      // fp64 noise bounds at the reference points, cap * 4
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -71,7 +76,44 @@ struct pdeval_ctx {
     bool timing = false;
     hipEvent_t ev[PDEVAL_N_PASSES + 1] = {};
     int ev_recorded = 0;
+    // the multi-GPU exchange (pdeval_comm_init)
+    ncclComm_t comm = nullptr;
+    int world = 1, rank = 0;
 };
+
+// RCCL, loaded on first use (dlopen: a process that already holds librccl.so.1, e.g. through
+// torch.distributed, shares that instance)
+namespace {
+struct Rccl {
+    bool tried = false;
+    void* h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+Rccl& rccl() {
+    static Rccl r;
+    if (!r.tried) {
+        r.tried = true;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (r.h) break;
+        }
+        if (r.h) {
+            r.get_unique_id = (decltype(r.get_unique_id))dlsym(r.h, "ncclGetUniqueId");
+            r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(r.h, "ncclCommInitRank");
+            r.all_gather = (decltype(r.all_gather))dlsym(r.h, "ncclAllGather");
+            r.comm_destroy = (decltype(r.comm_destroy))dlsym(r.h, "ncclCommDestroy");
+            r.error_string = (decltype(r.error_string))dlsym(r.h, "ncclGetErrorString");
+            if (!r.get_unique_id || !r.comm_init_rank || !r.all_gather || !r.comm_destroy || !r.error_string)
+                r.h = nullptr;
+        }
+    }
+    return r;
+}
+}  // namespace
 
 // in launch order (pass k lasts from event k to event k + 1)
 static const char* const kPassNames[PDEVAL_N_PASSES] = {
@@ -237,10 +279,12 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (!c) return PDEVAL_ERR_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->comm) pdeval_comm_destroy(c);
     for (int64_t* l : c->d_list)
         if (l) (void)hipFree(l);
     if (c->d_pstate) (void)hipFree(c->d_pstate);
     if (c->d_status) (void)hipFree(c->d_status);
+    if (c->d_noise) (void)hipFree(c->d_noise);
     for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) hipFree(p);
@@ -379,6 +423,9 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (c->d_status) (void)hipFree(c->d_status);
     c->d_status = nullptr;
     HIPCHK(c, hipMalloc(&c->d_status, cap));
+    if (c->d_noise) (void)hipFree(c->d_noise);
+    c->d_noise = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_noise, cap * 4 * sizeof(double)));
     c->cap = cap;
     return PDEVAL_OK;
 }
@@ -456,6 +503,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.pstate = c->d_pstate;
     a.pdeep_list = c->d_list[L_PDEEP];
     a.pdeep_count = cnt + L_PDEEP;
+    a.noise_ref = c->d_noise;
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
     // complex-valued ones -> L_CPLX
@@ -524,10 +572,14 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
                        dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, follow(L_ESC_DEEP2, -1, L_ESC));
     HIPCHK(c, hipGetLastError());
     if constexpr (FF) {
-        // (complex programs deeper than 4 keep their tier-1 class: 161 KiB of LDS would not fit)
         mark(10);
         hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4>), dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(64),
-                           (tier2_lds<cplx, K, 4>()), s, follow(L_ESC_C, -1, L_ESC_C));
+                           (tier2_lds<cplx, K, 4>()), s, follow(L_ESC_C, L_ESC_C_DEEP, L_ESC_C));
+        HIPCHK(c, hipGetLastError());
+        // complex programs of stack 5..8: operand stack in private memory (161 KiB of LDS would
+        // not fit)
+        hipLaunchKernelGGL((tier2_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>), dim3((unsigned)std::min<int64_t>(n, 256)),
+                           dim3(64), 0, s, follow(L_ESC_C_DEEP, -1, L_ESC_C));
         HIPCHK(c, hipGetLastError());
     } else {
         mark(10);
@@ -541,13 +593,16 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         b.defer_count = cnt + L_DD;
         b.cplx_list = c->d_list[L_DDC];
         b.cplx_count = cnt + L_DDC;
+        b.esc_list = c->d_list[L_DD8];
+        b.esc_count = cnt + L_DD8;
         hipLaunchKernelGGL(dd_collect_kernel<PROB>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b,
                            (const uint8_t*)a.out.status);
         HIPCHK(c, hipGetLastError());
         launch_dd_point(PROB, 0, lgrid, s, follow(L_DD, -1, L_ESC));
+        launch_dd_point(PROB, 1, lgrid, s, follow(L_DD8, -1, L_ESC));
         HIPCHK(c, hipGetLastError());
         if constexpr (FF) {
-            launch_dd_point(PROB, 1, lgrid, s, follow(L_DDC, -1, L_ESC));
+            launch_dd_point(PROB, 2, lgrid, s, follow(L_DDC, -1, L_ESC));
             HIPCHK(c, hipGetLastError());
         }
     }
@@ -561,6 +616,12 @@ extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64
                                       const pdeval_outputs* d_out, void* stream, int zero_bits) {
     if (!c || !d_out || n < 0 || (n > 0 && (!d_ops || !d_offsets)) || n_words < 0) {
         if (c) c->err = "pdeval_validate_device: bad argument";
+        return PDEVAL_ERR_ARG;
+    }
+    if (n > PDEVAL_MAX_BATCH) {
+        // work-list counters are int32 and candidate indices travel as 32-bit wave-uniform
+        // values: larger batches are split by the caller
+        c->err = "pdeval_validate_device: n exceeds PDEVAL_MAX_BATCH";
         return PDEVAL_ERR_ARG;
     }
     if (n == 0) return PDEVAL_OK;
@@ -583,6 +644,10 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
                                      pdeval_outputs* out) {
     if (!c || !out || n < 0 || (n > 0 && (!ops || !offsets))) {
         if (c) c->err = "pdeval_validate_batch: bad argument";
+        return PDEVAL_ERR_ARG;
+    }
+    if (n > PDEVAL_MAX_BATCH) {
+        c->err = "pdeval_validate_batch: n exceeds PDEVAL_MAX_BATCH";
         return PDEVAL_ERR_ARG;
     }
     if (n == 0) return PDEVAL_OK;
@@ -794,5 +859,72 @@ extern "C" int pdeval_point_eval(pdeval_ctx* c, const int32_t* prog, int64_t n_w
         c->err = std::string("pdeval_point_eval: ") + hipGetErrorString(e);
         return PDEVAL_ERR_HIP;
     }
+    return PDEVAL_OK;
+}
+
+// ---------------------------------------------------------------------------- multi-GPU
+extern "C" int pdeval_comm_unique_id(uint8_t* id) {
+    if (!id) return PDEVAL_ERR_ARG;
+    Rccl& r = rccl();
+    if (!r.h) {
+        g_err = "pdeval_comm_unique_id: librccl.so.1 not found";
+        return PDEVAL_ERR_NODEVICE;
+    }
+    ncclUniqueId u;
+    const ncclResult_t e = r.get_unique_id(&u);
+    if (e != ncclSuccess) {
+        g_err = std::string("ncclGetUniqueId: ") + r.error_string(e);
+        return PDEVAL_ERR_HIP;
+    }
+    std::memcpy(id, u.internal, PDEVAL_UNIQUE_ID_BYTES);
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_comm_init(pdeval_ctx* c, int world, int rank, const uint8_t* id) {
+    if (!c || !id || world < 1 || rank < 0 || rank >= world || c->comm) {
+        if (c) c->err = "pdeval_comm_init: bad argument (or already initialized)";
+        return PDEVAL_ERR_ARG;
+    }
+    Rccl& r = rccl();
+    if (!r.h) {
+        c->err = "pdeval_comm_init: librccl.so.1 not found";
+        return PDEVAL_ERR_NODEVICE;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, PDEVAL_UNIQUE_ID_BYTES);
+    const ncclResult_t e = r.comm_init_rank(&c->comm, world, u, rank);
+    if (e != ncclSuccess) {
+        c->comm = nullptr;
+        c->err = std::string("ncclCommInitRank: ") + r.error_string(e);
+        return PDEVAL_ERR_HIP;
+    }
+    c->world = world;
+    c->rank = rank;
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_gather_bits(pdeval_ctx* c, const uint8_t* d_local, int64_t nbytes, uint8_t* d_global,
+                                  void* stream) {
+    if (!c || !c->comm || !d_local || !d_global || nbytes <= 0) {
+        if (c) c->err = "pdeval_gather_bits: bad argument (pdeval_comm_init first)";
+        return PDEVAL_ERR_ARG;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    const ncclResult_t e = rccl().all_gather(d_local, d_global, (size_t)nbytes, ncclUint8, c->comm, s);
+    if (e != ncclSuccess) {
+        c->err = std::string("ncclAllGather: ") + rccl().error_string(e);
+        return PDEVAL_ERR_HIP;
+    }
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_comm_destroy(pdeval_ctx* c) {
+    if (!c) return PDEVAL_ERR_ARG;
+    if (c->comm && rccl().h) rccl().comm_destroy(c->comm);
+    c->comm = nullptr;
+    c->world = 1;
+    c->rank = 0;
     return PDEVAL_OK;
 }

@@ -54,6 +54,7 @@ struct KernelArgs {
     uint8_t* pstate;            // point-stage state per candidate (P0_*), or NULL
     int64_t* pdeep_list;        // real programs deeper than pass 0's stack: the deep point pass
     int32_t* pdeep_count;
+    double* noise_ref;          // n * n_ref fp64 noise bounds at the reference points (point stage)
 };
 
 // Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).

@@ -158,6 +158,8 @@ __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand
             return P0_NONE;
         }
         if (p == 0 && a.out.fingerprint) a.out.fingerprint[cand * PDEVAL_FP_N] = r.u0;
+        // the fp64 noise bound, reused (rescaled) by the double-double tier
+        if (!FINAL && a.noise_ref) a.noise_ref[cand * a.n_ref + p] = r.noise;
         // (a complex residual: its modulus with the sign of its real part)
         if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = r.res_im == 0.0 ? r.res_re : copysign(r.res_abs, r.res_re);
         if (!r.finite) {
@@ -314,18 +316,201 @@ __global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a, const uin
     const bool need = (ps & P0_DD) ||
                       ((ps & P0_PROV) && (st == PDEVAL_CLS_REJECT_GRID || st == PDEVAL_CLS_REJECT_SYMBOLIC));
     if (!need) return;
-    if (ps & P0_CPLX) list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
-    else list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
+    if (ps & P0_CPLX) {
+        list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
+    } else {
+        const int depth = (int)((a.ops[a.offsets[cand]] >> 8) & 0xff);
+        if (depth <= 2) list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
+        else list_append(a.esc_list, a.esc_count, a.list_capacity, cand);
+    }
 }
 
-// Tier B: the point stage in double-double (T = dd, or cdd for complex candidates), final.
-template <int PROB, class T>
-__global__ __launch_bounds__(64, 1) void dd_point_kernel(KernelArgs a) {
+// ---- the double-double tier's evaluator: values only.  Its noise bound is the fp64 one
+// rescaled from eps = 2^-52 to dd_unit() = 2^-100: the first-order error jets depend on the
+// magnitudes of the values (the same to first order in both precisions) and on the unit, so
+// the rescaled bound holds for the double-double evaluation (the coordinates' rounding term is
+// then 64x too large, which errs on the safe side).
+template <class T, int NC> struct LdsVStack {
+    T* vs;
+    int lane;
+    __device__ __forceinline__ void store(int slot, const T* t) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) vs[(slot * NC + c) * 64 + lane] = t[c];
+    }
+    __device__ __forceinline__ void load(int slot, T* t) const {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) t[c] = vs[(slot * NC + c) * 64 + lane];
+    }
+};
+template <class T, int NC, int SLOTS> struct PrivVStack {
+    T v[SLOTS][NC];
+    __device__ __forceinline__ void store(int slot, const T* t) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) v[slot][c] = t[c];
+    }
+    __device__ __forceinline__ void load(int slot, T* t) const {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) t[c] = v[slot][c];
+    }
+};
+
+// program words [pc, end) at (x, y) in jets over T with coordinates / constants of type V
+// (one candidate per lane: vector loads of the program)
+template <class T, int K, int MAXD, class V> struct ValInterp {
+    using O = JetOps<T, K>;
+    using J = typename O::J;
+    template <class STK>
+    static __device__ int run(const int32_t* ops, int pc, int end, V x, V y, J& acc, STK& stk) {
+        int d = 0;
+        if (pc >= end) return RUN_BAD;
+        for (;;) {
+            const uint32_t w = (uint32_t)ops[pc];
+            const uint32_t op = w & 0xffu;
+            V immv = vzero<V>();
+            int npc = pc + 1;
+            if (op_has_imm(op)) {
+                npc = pc + ((w & PDEVAL_IMM_DD) ? 5 : 3);
+                if (npc > end) return RUN_BAD;
+                immv = read_imm<V, true>(ops + pc + 1, w);
+            }
+            switch (op) {
+                case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I:
+                    if (d > 0 && d < MAXD) stk.store(d - 1, acc.c);
+                    if (op == PDOP_PUSH_X) O::set_var(acc, x, 0);
+                    else if (op == PDOP_PUSH_Y) O::set_var(acc, y, 1);
+                    else if (op == PDOP_PUSH_C) O::set_const(acc, cvt<T>(immv));
+                    else {
+                        if constexpr (Real<T>::cplx_pass) O::set_const(acc, imag_unit<T>());
+                        else return RUN_UNSUPPORTED;
+                    }
+                    ++d;
+                    break;
+                case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB:
+                case PDOP_MUL: case PDOP_DIV: case PDOP_RDIV:
+                    if (d >= 2 && d <= MAXD) {
+                        J lhs;
+                        stk.load(d - 2, lhs.c);
+                        Interp<T, K, MAXD>::binop(op, lhs, acc);
+                    }
+                    --d;
+                    break;
+                case PDOP_ADDC: acc.c[0] = acc.c[0] + cvt<T>(immv); break;
+                case PDOP_MULC: O::scale(acc, cvt<T>(immv)); break;
+                case PDOP_RDIVC: O::rdivc(acc, cvt<T>(immv)); break;
+                case PDOP_PUSH_P: case PDOP_ADD_P: case PDOP_SUB_P: case PDOP_MUL_P: case PDOP_DIV_P:
+                case PDOP_RDIV_P: {
+                    V pk[K + 1];
+                    const int n = (int)((w >> 8) & 0xffu);
+                    if (op == PDOP_PUSH_P && d > 0 && d < MAXD) stk.store(d - 1, acc.c);
+                    if ((w >> 16) & 1) {
+                        O::pcoefs(y, n, pk);
+                        if (op == PDOP_PUSH_P) O::template set_p<1>(acc, pk);
+                        else O::template p_op<1>(op, acc, pk);
+                    } else {
+                        O::pcoefs(x, n, pk);
+                        if (op == PDOP_PUSH_P) O::template set_p<0>(acc, pk);
+                        else O::template p_op<0>(op, acc, pk);
+                    }
+                    if (op == PDOP_PUSH_P) ++d;
+                    break;
+                }
+                case PDOP_NEG: O::scale(acc, from_real<T>(-1.0)); break;
+                case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: {
+                    const bool isx = (op == PDOP_ADD_X || op == PDOP_SUB_X);
+                    const double sg = (op == PDOP_ADD_X || op == PDOP_ADD_Y) ? 1.0 : -1.0;
+                    acc.c[0] = acc.c[0] + cvt<T>((isx ? x : y) * sg);
+                    const int idx = isx ? ji(1, 0) : ji(0, 1);
+                    acc.c[idx] = acc.c[idx] + from_real<T>(sg);
+                    break;
+                }
+                case PDOP_MUL_X: O::mul_var(acc, x, 0); break;
+                case PDOP_MUL_Y: O::mul_var(acc, y, 1); break;
+                case PDOP_DIV_X: O::div_var(acc, x, 0); break;
+                case PDOP_DIV_Y: O::div_var(acc, y, 1); break;
+                case PDOP_POWN: O::pown(acc, (int)((w >> 8) & 0xffu)); break;
+                case PDOP_POW: O::powa(acc, hi_of(immv)); break;
+                case PDOP_SQRT: O::sqrtj(acc); break;
+                case PDOP_EXP: O::expj(acc); break;
+                case PDOP_LOG: O::logj(acc); break;
+                case PDOP_ABS: absj<K>(acc); break;
+                default: return RUN_UNSUPPORTED;
+            }
+            if (npc >= end) break;
+            pc = npc;
+        }
+        return d == 1 ? RUN_OK : RUN_BAD;
+    }
+};
+
+// The double-double tier for one candidate: values at every reference point, the rescaled
+// fp64 noise bounds, the final rule; writes res_ref and q_ref.  Returns the P0_* class bits
+// (P0_NONE: not evaluated -- program error or not finite, the fp64 decision stands).
+template <int PROB, class T, int MAXD, class STK>
+__device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t cand, const int32_t* prog, int plen,
+                                                  uint32_t hdr, STK& stk) {
+    constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+    constexpr int NC = nc(K);
+    double qr = 0.0;
+    bool rej = false, fin_all = true;
+    uint8_t ff = P0_PASS;
+    for (int p = 0; p < a.n_ref; ++p) {
+        const dd x = a.ref_xd[p & 3], y = a.ref_yd[p & 3];
+        typename ValInterp<T, K, MAXD, dd>::J u;
+        if (ValInterp<T, K, MAXD, dd>::run(prog, 1, plen, x, y, u, stk) != RUN_OK) return P0_NONE;
+        double m[NC];
+#pragma unroll
+        for (int i = 0; i < NC; ++i) m[i] = mag(u.c[i]);
+        T res;
+        double S;
+        if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+            res = FFEpi<T, false>::eval(u.c, x);
+            S = FFEpi<double, true>::eval(m, x.hi);
+        } else {
+            res = kerr_lhs<T, dd>(u.c, a.kc_ref + 4 * p, &S);
+        }
+        const double res_abs = mag(res);
+        const double noise = a.noise_ref[cand * a.n_ref + p] * (dd_unit() / kEps);
+        bool fin = finite_(res) && isfinite(S) && isfinite(noise);
+#pragma unroll
+        for (int i = 0; i < NC; ++i) fin = fin && m[i] < kHugeJet;
+        const double rr = re_hi(res), ri = im_hi(res);
+        if (isfinite(res_abs) && a.out.res_ref)
+            a.out.res_ref[cand * a.n_ref + p] = ri == 0.0 ? rr : copysign(res_abs, rr);
+        if (!fin) {
+            fin_all = false;
+            continue;
+        }
+        if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+            qr = scaled(res_abs, S);
+            ff = ff_point_rule<true>(res_abs, noise, (hdr & PDEVAL_FLAG_RATIONAL) != 0, a.prm);
+        } else {
+            qr = fmax(qr, res_abs);
+            rej = rej || kerr_point_rule<true>(res_abs, noise, a.prm) == 1;
+        }
+    }
+    if (!fin_all) return P0_NONE;
+    if (a.out.q_ref) a.out.q_ref[cand] = qr;
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) return ff & 3;
+    else return rej ? P0_REJECT : P0_PASS;
+}
+
+// Tier B: the point stage in double-double (T = dd, or cdd for complex candidates), final,
+// one candidate per lane over a device list.  MAXD = 2: operand stack in LDS (the common
+// case); deeper or complex programs: private memory.
+template <int PROB, class T, int MAXD>
+__global__ __launch_bounds__(64, MAXD == 2 ? 2 : 1) void dd_point_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
-    constexpr int MAXD = PDEVAL_MAX_STACK;
+    constexpr int NC = nc(K);
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
-    PrivStack<T, nc(K), MAXD - 1> stk;
+#ifndef PD_HOST_SIM
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
+    using STK = typename std::conditional<MAXD == 2, LdsVStack<T, NC>, PrivVStack<T, NC, MAXD - 1>>::type;
+    STK stk;
+    if constexpr (MAXD == 2) stk = STK{reinterpret_cast<T*>(pd_lds), (int)(threadIdx.x & 63)};
     for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwork;
          wi += (int64_t)gridDim.x * blockDim.x) {
         const int64_t cand = a.list[wi];
@@ -333,10 +518,9 @@ __global__ __launch_bounds__(64, 1) void dd_point_kernel(KernelArgs a) {
         if (!prog_bounds(a, cand, &beg, &end)) continue;
         const int32_t* prog = a.ops + beg;
         const uint32_t hdr = (uint32_t)prog[0];
-        bool nf, perr;
-        const uint8_t s = point_stage<PROB, T, dd, MAXD, true, true>(a, cand, prog, (int)(end - beg), hdr, stk,
-                                                                    &nf, &perr);
-        if (perr || nf) continue;   // (finite in fp64: keep the fp64 decision)
+        if ((int)((hdr >> 8) & 0xffu) > MAXD) continue;     // (the collect pass routes by depth)
+        const uint8_t s = dd_point_stage<PROB, T, MAXD>(a, cand, prog, (int)(end - beg), hdr, stk);
+        if (s == P0_NONE) continue;   // not finite: keep the fp64 decision
         const uint8_t st = a.out.status ? a.out.status[cand] : (uint8_t)PDEVAL_CLS_ACCEPT;
         // the reference checks the gradient (and Kerr the constant) before the point stage
         const bool overridable = st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||

@@ -16,12 +16,16 @@ void launch_point_list(int problem, int cplx, unsigned grid, hipStream_t s, cons
     }
 }
 
-void launch_dd_point(int problem, int cplx, unsigned grid, hipStream_t s, const KernelArgs& a) {
-    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
-        if (cplx) hipLaunchKernelGGL((dd_point_kernel<PDEVAL_PROBLEM_FORCE_FREE, cdd>), dim3(grid), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL((dd_point_kernel<PDEVAL_PROBLEM_FORCE_FREE, dd>), dim3(grid), dim3(64), 0, s, a);
+void launch_dd_point(int problem, int kind, unsigned grid, hipStream_t s, const KernelArgs& a) {
+    constexpr int FF = PDEVAL_PROBLEM_FORCE_FREE, KR = PDEVAL_PROBLEM_KERR;
+    const size_t lds_ff = (size_t)nc(4) * 64 * sizeof(dd), lds_kr = (size_t)nc(2) * 64 * sizeof(dd);
+    if (problem == FF) {
+        if (kind == 0) hipLaunchKernelGGL((dd_point_kernel<FF, dd, 2>), dim3(grid), dim3(64), lds_ff, s, a);
+        else if (kind == 1) hipLaunchKernelGGL((dd_point_kernel<FF, dd, PDEVAL_MAX_STACK>), dim3(grid), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((dd_point_kernel<FF, cdd, PDEVAL_MAX_STACK>), dim3(grid), dim3(64), 0, s, a);
     } else {
-        hipLaunchKernelGGL((dd_point_kernel<PDEVAL_PROBLEM_KERR, dd>), dim3(grid), dim3(64), 0, s, a);
+        if (kind == 0) hipLaunchKernelGGL((dd_point_kernel<KR, dd, 2>), dim3(grid), dim3(64), lds_kr, s, a);
+        else if (kind == 1) hipLaunchKernelGGL((dd_point_kernel<KR, dd, PDEVAL_MAX_STACK>), dim3(grid), dim3(64), 0, s, a);
     }
 }
 

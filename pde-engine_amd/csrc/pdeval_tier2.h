@@ -436,7 +436,9 @@ template <int PROB, class T> __device__ __forceinline__ double residual_noise(co
 #ifndef PD_T2_WAVES_PER_SIMD
 #define PD_T2_WAVES_PER_SIMD 1   // 512 registers: no spills
 #endif
-template <int PROB, class T, int MAXD>
+// PRIV: the operand stack in private memory instead of LDS (complex programs of stack 5..8,
+// whose value + error slots would need 161 KiB of LDS per wave)
+template <int PROB, class T, int MAXD, bool PRIV = false>
 __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
     constexpr int NC = nc(K);
@@ -450,6 +452,9 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
 #endif
     T* vs = reinterpret_cast<T*>(pd_lds);
     double* es = reinterpret_cast<double*>(pd_lds + (size_t)(MAXD - 1) * NC * 64 * sizeof(T));
+    using STK = typename std::conditional<PRIV, PrivStack<T, NC, MAXD - 1>, LdsStack<T, NC>>::type;
+    STK stk;
+    if constexpr (!PRIV) stk = STK{vs, es, lane};
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
     for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
@@ -475,7 +480,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             const double y = l == 0 ? a.ref_y[0] : (l == 1 ? a.ref_y[1] : (l == 2 ? a.ref_y[2] : a.ref_y[3]));
             J u;
             double e[NC];
-            const int rc = I::run(prog, 1, plen, x, y, u, e, vs, es, lane);
+            const int rc = I::template run_s<false>(prog, 1, plen, x, y, u, e, stk);
             bool real_fail = rc != RUN_OK;
             if (rc == RUN_OK) {
                 const double* kc = a.kc ? a.kc + 4 * l : nullptr;
@@ -505,7 +510,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
                 const double y = a.gy[sl * 64 + lane];
                 J u;
                 double e[NC];
-                const int rc = I::run(prog, 1, plen, x, y, u, e, vs, es, lane);
+                const int rc = I::template run_s<false>(prog, 1, plen, x, y, u, e, stk);
                 if (rc != RUN_OK) { ++nnonfin; continue; }
                 const double* kc = a.kc ? a.kc + 4 * p : nullptr;
                 PointResult r;

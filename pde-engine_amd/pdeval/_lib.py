@@ -24,9 +24,13 @@ EXPORTS = (
     'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
     'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts', 'pdeval_eval_points',
     'pdeval_compile_batch', 'pdeval_canonical', 'pdeval_point_eval', 'pdeval_point_states',
+    'pdeval_comm_unique_id', 'pdeval_comm_init', 'pdeval_gather_bits', 'pdeval_comm_destroy',
 )
+MAX_BATCH = 1 << 30          # PDEVAL_MAX_BATCH
+UNIQUE_ID_BYTES = 128
 LIST_NAMES = ('defer_stack3', 'complex', 'defer_stack8', 'tier2', 'tier2_stack3', 'tier2_complex',
-              'complex_stack8', 'tier2_stack8', 'point_deep', 'point_dd', 'point_dd_complex')
+              'complex_stack8', 'tier2_stack8', 'point_deep', 'point_dd', 'point_dd_complex',
+              'point_dd_stack8', 'tier2_complex_stack8')
 N_PASSES = 12
 
 
@@ -83,6 +87,10 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_canonical.argtypes = [C.c_int, C.c_char_p, i64, C.c_char_p, i64]
     lib.pdeval_point_eval.argtypes = [vp, vp, i64, C.c_int, vp, vp]
     lib.pdeval_point_states.argtypes = [vp, vp, i64]
+    lib.pdeval_comm_unique_id.argtypes = [vp]
+    lib.pdeval_comm_init.argtypes = [vp, C.c_int, C.c_int, vp]
+    lib.pdeval_gather_bits.argtypes = [vp, vp, i64, vp, vp]
+    lib.pdeval_comm_destroy.argtypes = [vp]
     for name in EXPORTS:
         getattr(lib, name)   # every symbol of the header must resolve
     if path is None:
@@ -201,6 +209,19 @@ class Context:
         _check(self.h, self.lib.pdeval_point_states(self.h, _ptr(out), n))
         return out
 
+    # ---- multi-GPU exchange (RCCL through the C ABI)
+    def comm_init(self, world: int, rank: int, unique_id: bytes):
+        """Join the RCCL communicator of `world` ranks (collective; same id on every rank)."""
+        buf = C.create_string_buffer(bytes(unique_id), UNIQUE_ID_BYTES)
+        _check(self.h, self.lib.pdeval_comm_init(self.h, world, rank, buf))
+
+    def gather_bits(self, d_local: int, nbytes: int, d_global: int, stream: int = 0):
+        """All-gather nbytes of device memory from every rank into d_global (world * nbytes)."""
+        _check(self.h, self.lib.pdeval_gather_bits(self.h, d_local, nbytes, d_global, stream or None))
+
+    def comm_destroy(self):
+        _check(self.h, self.lib.pdeval_comm_destroy(self.h))
+
     def pass_counts(self):
         """{work list: entries} of the most recent call (synchronizes)."""
         c = (C.c_int64 * len(LIST_NAMES))()
@@ -216,6 +237,15 @@ class Context:
         rc = self.lib.pdeval_validate_device(self.h, d_ops, n_words, d_offsets, n, C.byref(prm),
                                              C.byref(d_out), stream, int(zero_bits))
         _check(self.h, rc)
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (on one rank; share it with the others)."""
+    buf = C.create_string_buffer(UNIQUE_ID_BYTES)
+    rc = load().pdeval_comm_unique_id(buf)
+    if rc != 0:
+        raise PdevalError(f'pdeval_comm_unique_id failed ({rc}): {load().pdeval_last_error(None).decode()}')
+    return buf.raw
 
 
 def program_depth(words: np.ndarray) -> int:

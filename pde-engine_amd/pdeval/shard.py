@@ -2,10 +2,11 @@
 
 The reference's only parallelism is N validator processes pulling ``(expr_id, expr_str)``
 from one ``multiprocessing.Queue`` (``general_method_paper_reproduction.py:773-823``).  Here a
-batch is split into contiguous ranges, one per rank (one process per GPU); every rank
-validates its range with no data-path communication, and the packed verdict bitmaps are then
-assembled on every rank with a single all-gather (RCCL over xGMI on the GPU box, gloo in the
-CPU tests).
+batch is split into contiguous ranges, one per rank (one process per GPU), balanced by the
+programs' FLOP model; every rank validates its range with no data-path communication, and the
+packed verdict bitmaps are then assembled on every rank with a single all-gather: natively
+through the C ABI (``pdeval_gather_bits``, RCCL over xGMI, :func:`gather_verdicts_native`) or
+through ``torch.distributed`` (:func:`gather_verdicts`; gloo in the CPU tests).
 """
 from __future__ import annotations
 
@@ -81,5 +82,34 @@ def gather_verdicts(local_bits, ranges: Sequence[Tuple[int, int]], group=None):
         parts = [torch.empty_like(buf) for _ in range(world)]
         dist.all_gather(parts, buf, group=group)
         out = torch.cat(parts)
+    host = out.cpu().numpy().reshape(world, nbytes)
+    return np.concatenate([unpack_bits(host[r], e - s) for r, (s, e) in enumerate(ranges)])
+
+
+def init_native_comm(ctx, rank: int, world: int, group=None):
+    """Join every rank's libpdeval context into one RCCL communicator: rank 0 draws the
+    unique id, torch.distributed carries it to the others (a 128-byte broadcast, once)."""
+    import torch.distributed as dist
+    from ._lib import comm_unique_id
+    box = [comm_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(box, src=0, group=group)
+    ctx.comm_init(world, rank, box[0])
+
+
+def gather_verdicts_native(ctx, local_bits, ranges: Sequence[Tuple[int, int]], stream: int = 0):
+    """The same all-gather as :func:`gather_verdicts`, through ``pdeval_gather_bits`` (one
+    ``ncclAllGather`` of the padded per-rank bitmaps on the context's communicator).
+    ``local_bits`` is this rank's packed bitmap as a uint8 torch tensor on the context's GPU."""
+    import torch
+    world = len(ranges)
+    nbytes = max(max(((e - s) + 7) // 8 for s, e in ranges), 1)
+    buf = torch.zeros(nbytes, dtype=torch.uint8, device=local_bits.device)
+    k = min(nbytes, local_bits.numel())
+    buf[:k] = local_bits.reshape(-1)[:k]
+    out = torch.empty(world * nbytes, dtype=torch.uint8, device=local_bits.device)
+    torch.cuda.synchronize(local_bits.device)
+    ctx.gather_bits(buf.data_ptr(), nbytes, out.data_ptr(), stream)
+    torch.cuda.synchronize(local_bits.device)
     host = out.cpu().numpy().reshape(world, nbytes)
     return np.concatenate([unpack_bits(host[r], e - s) for r, (s, e) in enumerate(ranges)])

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# torch first: its bundled HIP runtime must be the one the process loads before libpdeval.so
+# (which then binds to the already-loaded libamdhip64 of the same soname); the GPU tests that
+# hand torch device buffers to the C ABI need torch to see the GPUs
+import torch  # noqa: E402,F401
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, 'pde-engine_amd'), os.path.join(ROOT, 'tests'), ROOT):
     if p not in sys.path:

@@ -313,3 +313,82 @@ def test_native_compile_full_kerr_d3(kerr_ctx):
     ref = kerr_ctx.validate(d['ops'], d['offsets'])
     diff = np.flatnonzero(nat['status'] != ref['status'])
     assert not diff.size, [(strings[i], int(nat['status'][i]), int(ref['status'][i])) for i in diff[:10]]
+
+
+def test_validate_device_limits_and_bad_programs(ff_ctx):
+    """pdeval_validate_device on device buffers: a batch beyond PDEVAL_MAX_BATCH is refused
+    (PDEVAL_ERR_ARG, nothing launched); a program whose offsets leave the ops array is
+    classified BAD_PROGRAM without being dereferenced; an UNSUPPORTED opcode gives
+    UNSUPPORTED; the good programs around them keep their classes."""
+    import torch
+    from pdeval import _lib
+    pd_ = P.force_free()
+    progs = [pd_.compile(pd_.parse(s)) for s in ('rho*z', 'rho**2')] + [P.UNSUPPORTED_PROGRAM]
+    ops, off = P.pack(progs)
+    off = np.concatenate([off, [off[-1] + 1000]])          # a 4th program past the end of ops
+    dev = torch.device('cuda:0')
+    d_ops = torch.from_numpy(ops).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    n = len(off) - 1
+    outs = dict(verdict_bits=torch.zeros(4, dtype=torch.uint8, device=dev),
+                status=torch.full((n,), 255, dtype=torch.uint8, device=dev),
+                q_ref=torch.zeros(n, dtype=torch.float64, device=dev),
+                res_ref=torch.zeros(n, dtype=torch.float64, device=dev),
+                q_grid=torch.zeros(n, dtype=torch.float64, device=dev),
+                n_bad=torch.zeros(n, dtype=torch.int32, device=dev),
+                n_nonfinite=torch.zeros(n, dtype=torch.int32, device=dev),
+                fingerprint=torch.zeros(4 * n, dtype=torch.float64, device=dev))
+    d_out = _lib.Outputs(*[outs[f].data_ptr() for f, _ in _lib.Outputs._fields_])
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    with pytest.raises(_lib.PdevalError, match='PDEVAL_MAX_BATCH'):
+        ff_ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), _lib.MAX_BATCH + 1, d_out,
+                               stream=stream.cuda_stream)
+    ff_ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out,
+                           stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    st = outs['status'].cpu().numpy()
+    assert st.tolist() == [1, 0, 5, 6], st           # reject, accept, UNSUPPORTED, BAD_PROGRAM
+    bits = np.unpackbits(outs['verdict_bits'].cpu().numpy(), bitorder='little')[:n]
+    assert bits.tolist() == [0, 1, 0, 0]
+
+
+def test_sharded_chain_world1_native_and_torch_gather():
+    """The multi-GPU chain at world size 1 on the GPU: shard_ranges -> validate_device on
+    the shard -> the one all-gather, both through the C ABI's RCCL communicator
+    (pdeval_gather_bits) and through torch.distributed (gloo), equal to the unsharded bitmap."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from pdeval import _lib
+    from pdeval.shard import gather_verdicts, gather_verdicts_native, init_native_comm, shard_ranges
+    pd_ = P.force_free()
+    rows = G.decided(G.ref_rows(*G.FF_REF))
+    ops, off, _ = P.compile_strings(pd_, [r['expr'] for r in rows])
+    ctx = Context(0)
+    ref = ctx.validate(ops, off)
+    with socket.socket() as s_:
+        s_.bind(('127.0.0.1', 0))
+        port = s_.getsockname()[1]
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=0, world_size=1)
+    try:
+        ranges = shard_ranges(len(rows), 1, weights=np.diff(off).astype(float))
+        assert ranges == [(0, len(rows))]
+        dev = torch.device('cuda:0')
+        d_ops = torch.from_numpy(ops).to(dev)
+        d_off = torch.from_numpy(off).to(dev)
+        n = len(rows)
+        bits = torch.zeros(((n + 31) // 32) * 4, dtype=torch.uint8, device=dev)
+        d_out = _lib.Outputs(bits.data_ptr(), None, None, None, None, None, None, None)
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.synchronize(dev)
+        ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out, stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        via_torch = gather_verdicts(bits.cpu(), ranges)
+        init_native_comm(ctx, 0, 1)
+        via_rccl = gather_verdicts_native(ctx, bits, ranges)
+        assert np.array_equal(via_torch, ref['verdict'])
+        assert np.array_equal(via_rccl, ref['verdict'])
+    finally:
+        dist.destroy_process_group()
+        ctx.close()
