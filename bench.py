@@ -84,6 +84,10 @@ def main():
                     help='headline run stops after the point stage for point-rejects')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='CPU-baseline time budget')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--sympy-seconds', type=float, default=100.0,
+                    help='wall budget of the SymPy CPU leg (the north star\'s CPU baseline)')
+    ap.add_argument('--cpu-procs', type=int, default=0,
+                    help='host processes of the SymPy leg (0: OMP_NUM_THREADS, the box\'s CPU share)')
     ap.add_argument('--no-extras', action='store_true',
                     help='skip the early-exit / host-buffer / time-to-solutions legs')
     a = ap.parse_args()
@@ -302,13 +306,65 @@ def main():
                 'native_only_s': round(t_nat, 4), 'native_strings_per_s': round(len(strs) / t_nat),
                 'hybrid_compile_s': round(t_comp, 4)}
 
+    if not a.no_extras and world == 1 and pid == PROBLEM_FORCE_FREE:
+        # the worker pool's batch path, queue tuples in -> result tuples out (the reference's
+        # _parallel_validator_worker protocol, general_method_paper_reproduction.py:1756-1816)
+        res['worker_process_batch'] = worker_throughput(exprs_all)
+
     if rank == 0:
         if not a.no_cpu and world == 1:
-            res['cpu_baseline'] = cpu_baseline(pid, ops_all, off_all, idx, a.cpu_seconds)
+            procs = a.cpu_procs or int(os.environ.get('OMP_NUM_THREADS', '0') or os.cpu_count())
+            if pid == PROBLEM_FORCE_FREE:
+                res['cpu_baseline'] = cpu_baseline_sympy(procs, a.sympy_seconds)
+            res['cpu_baseline_c_port'] = cpu_baseline(pid, ops_all, off_all, idx, a.cpu_seconds)
         print(json.dumps(res))
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def worker_throughput(exprs, batch=4096):
+    """process_batch (pdeval/worker.py) over every validated d4 string in queue-sized batches:
+    native compile, one device call, known-solution tags; candidates/s end to end."""
+    from problems import load_problem
+    from pdeval.worker import KnownSolutionTagger, filtered_kwargs, process_batch
+    prob = load_problem('force_free')
+    locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
+    tagger = KnownSolutionTagger(prob, locs)
+    kw = filtered_kwargs(prob.validator)
+    items = [(i + 1, str(s)) for i, s in enumerate(exprs)]
+    process_batch(items[:batch], prob.validator, kw, locs, tagger)      # warm
+    t0 = time.perf_counter()
+    n_valid = n_tag = 0
+    for k in range(0, len(items), batch):
+        out = process_batch(items[k:k + batch], prob.validator, kw, locs, tagger)
+        n_valid += sum(1 for t in out if t[1])
+        n_tag += sum(1 for t in out if t[3])
+    dt = time.perf_counter() - t0
+    return {'candidates': len(items), 'batch': batch, 'seconds': round(dt, 3),
+            'candidates_per_s': round(len(items) / dt), 'valid': n_valid, 'paper_tagged': n_tag}
+
+
+def cpu_baseline_sympy(procs, budget_s):
+    """The SymPy CPU path (oracle/sympy_validator.py, the reference's validate restated) on
+    the host cores: C1 (the 111 depth<=2 candidates that reach validate) then a seed-0 sample
+    of 1,000 depth-4 ones, 60 s per-candidate timeout, wall budget budget_s."""
+    import gzip
+    import random
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import sympy_bench
+    with gzip.open(os.path.join(ROOT, 'tests', 'golden', 'streams', 'force_free_d3_validated.txt.gz'), 'rt') as f:
+        c1 = [l.rstrip('\n').split('\t')[-1] for l in f if int(l.split('\t')[-2]) <= 2]
+    with gzip.open(os.path.join(ROOT, 'tests', 'golden', 'streams', 'force_free_d4_validated.txt.gz'), 'rt') as f:
+        d4 = [l.rstrip('\n').split('\t')[-1] for l in f]
+    d4s = random.Random(0).sample(d4, 1000)
+    r = sympy_bench.run(c1 + d4s, procs, timeout=60, budget_s=budget_s)
+    return {'value': r['rate_completed'], 'unit': 'candidates/s', 'cores': procs, 'kind': 'port',
+            'sample': (f"SymPy restatement of the reference's validate (oracle/sympy_validator.py), "
+                       f"multiprocessing.Pool({procs}), 60 s per-candidate timeout, on C1 ({len(c1)} "
+                       f"depth<=2 candidates) then a seed-0 sample of 1,000 depth-4 candidates, "
+                       f"{budget_s:.0f} s wall budget"),
+            'detail': r}
 
 
 def cpu_baseline(pid, ops_all, off_all, idx, budget_s):

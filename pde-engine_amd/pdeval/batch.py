@@ -128,14 +128,15 @@ class BatchValidator:
                                tuple(float(v) for v in r['fingerprint'][i])))
         return out
 
-    def validate_strings(self, strings: Sequence[str]) -> List[Verdict]:
+    def validate_strings(self, strings: Sequence[str], stats: Optional[dict] = None) -> List[Verdict]:
         """Candidate strings in: compiled by the native compiler (csrc/pdcompile.cpp), SymPy
         only for the strings it declines (pdeval/native.py); unparsable strings get the
-        UNSUPPORTED stub and an "Error: ..." reason, as on the SymPy path."""
+        UNSUPPORTED stub and an "Error: ..." reason, as on the SymPy path.  ``stats`` receives
+        the compile statistics and the native per-string status (native.compile_strings)."""
         if not strings:
             return []
         from .native import compile_strings
-        ops, off, notes = compile_strings(self.pd, list(strings))
+        ops, off, notes = compile_strings(self.pd, list(strings), stats=stats)
         return self._verdicts(ops, off, notes)
 
     def close(self):

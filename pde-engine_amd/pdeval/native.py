@@ -56,12 +56,14 @@ def compile_native(problem_id: int, strings: Sequence[str]):
 
 def compile_strings(pd_, strings: Sequence[str], stats: Optional[dict] = None):
     """Drop-in for ``problem_defs.compile_strings``: native compile, SymPy for the rest.
-    Returns (ops, offsets, notes) with notes[i] = None or the reason a program is a stub."""
+    Returns (ops, offsets, notes) with notes[i] = None or the reason a program is a stub.
+    With a ``stats`` dict, ``stats['status']`` receives the native compiler's per-string
+    status (COMPILE_PARSE marks the strings it could not parse)."""
     from .problem_defs import compile_strings as sympy_compile
     ops, off, st = compile_native(pd_.problem_id, strings)
     host = np.flatnonzero(st != COMPILE_OK)
     if stats is not None:
-        stats.update(n=len(strings), native=int(len(strings) - len(host)), host=int(len(host)))
+        stats.update(n=len(strings), native=int(len(strings) - len(host)), host=int(len(host)), status=st)
     notes: List[Optional[str]] = [None] * len(strings)
     if len(host) == 0:
         return ops, off, notes

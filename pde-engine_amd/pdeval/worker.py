@@ -63,11 +63,15 @@ class KnownSolutionTagger:
     def fingerprints(self, us: Sequence[sp.Basic]) -> np.ndarray:
         return np.array([v.fingerprint for v in self.bv.validate_exprs(list(us))])
 
-    def tag(self, us: Sequence[sp.Basic]) -> List[Tuple[bool, Optional[str]]]:
+    def tag(self, us: Sequence[sp.Basic], fps: Optional[np.ndarray] = None) -> List[Tuple[bool, Optional[str]]]:
+        """Known-solution tags of valid rows.  ``us``: SymPy trees, or strings (parsed only
+        when their fingerprint matches); ``fps``: their fingerprints from the validation call
+        that accepted them (validated again on the device when not given)."""
         out: List[Tuple[bool, Optional[str]]] = [(False, None)] * len(us)
         if not self.known or not len(us):
             return out
-        fp = self.fingerprints(us)
+        fp = np.asarray(fps) if fps is not None else self.fingerprints(
+            [sp.sympify(u, locals=self.locals) if isinstance(u, str) else u for u in us])
         for i, u in enumerate(us):
             for k, (ke, name) in enumerate(self.known):
                 a, b = fp[i], self.fps[k]
@@ -75,7 +79,8 @@ class KnownSolutionTagger:
                 if fin.sum() < 2 or not np.allclose(a[fin], b[fin], rtol=self.rtol, atol=1e-12):
                     continue
                 try:
-                    if sp.simplify(u - ke) == 0:        # the reference's test, :1791
+                    ue = sp.sympify(u, locals=self.locals) if isinstance(u, str) else u
+                    if sp.simplify(ue - ke) == 0:        # the reference's test, :1791
                         out[i] = (True, name)
                         break
                 except Exception:   # noqa: BLE001
@@ -180,27 +185,30 @@ def process_batch(claimed, validator, kwargs, locs, tagger):
 
 
 def _process_batch_strings(claimed, validator, locs, tagger):
-    """Fast path of process_batch: the strings go to the native compiler, SymPy parses only
-    what it cannot (declined strings, parse errors -- whose message the reference reports as
-    'Validator Error: ...', :1703-1714) and the accepted rows (known-solution tagging)."""
-    from .native import COMPILE_PARSE, compile_native
-    pid = validator._validator().problem_id
-    _, _, st = compile_native(pid, [s for _, s in claimed])
-    results, ids, strs = [], [], []
-    for (expr_id, expr_str), t in zip(claimed, st):
-        if t == COMPILE_PARSE:
+    """Fast path of process_batch: one native compile of the batch (SymPy only for the
+    strings the native compiler declines), one device call, and the known-solution tags
+    from that call's fingerprints -- SymPy parses only parse errors (whose message the
+    reference reports as 'Validator Error: ...', :1703-1714) and fingerprint hits (the
+    reference's simplify(u - known) == 0, :1785-1798)."""
+    from .native import COMPILE_PARSE
+    bv = validator._validator()
+    strs = [s for _, s in claimed]
+    stats: dict = {}
+    verdicts = bv.validate_strings(strs, stats=stats)
+    st = stats.get('status')
+    results, keep = [], []
+    for i, (expr_id, expr_str) in enumerate(claimed):
+        if st is not None and st[i] == COMPILE_PARSE:
             try:
                 sp.sympify(expr_str, locals=locs)
             except Exception as e:   # noqa: BLE001
                 results.append(('error', None, f'Validator Error: {e}', None, None, expr_id))
                 continue
-        ids.append(expr_id)
-        strs.append(expr_str)
-    if strs:
-        verdicts = validator.validate_strings(strs)
-        valid = [i for i, (ok, _) in enumerate(verdicts) if ok]
-        tags = dict(zip(valid, tagger.tag([sp.sympify(strs[i], locals=locs) for i in valid])))
-        for i, (ok, reason) in enumerate(verdicts):
-            is_paper, name = tags.get(i, (False, None))
-            results.append(('completed', bool(ok), reason, is_paper, name, ids[i]))
+        keep.append(i)
+    valid = [i for i in keep if verdicts[i].ok]
+    tags = dict(zip(valid, tagger.tag([strs[i] for i in valid],
+                                      fps=np.array([verdicts[i].fingerprint for i in valid]).reshape(-1, 4))))
+    for i in keep:
+        is_paper, name = tags.get(i, (False, None))
+        results.append(('completed', bool(verdicts[i].ok), verdicts[i].reason, is_paper, name, claimed[i][0]))
     return results

@@ -71,3 +71,40 @@ def _slow(claimed, validator, kw, locs, tagger):
         t = tags.get(i, (False, None))
         out.append(('completed', bool(ok), reason, t[0], t[1], ids[i]))
     return out
+
+
+def test_worker_with_run_database_and_writer(tmp_path):
+    """End to end on the GPU: candidates INSERTed 'pending' into a run table with the
+    reference's schema, the GPU worker claims them from the database (compare-and-set claims,
+    :1736-1751), the centralized writer applies its result tuples (:1178-1204), and the report
+    --print-run-id prints (_generate_report_from_db) has the reference's valid count and the
+    paper solutions of the fixtures."""
+    import hashlib
+    import os
+    import threading
+    from pdeval import persist
+    from pdeval.worker import validator_worker
+    rows = G.decided(G.ref_rows('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_edge.jsonl'))
+    db = os.path.join(tmp_path, 'run.db')
+    run_id = 'gpu-run'
+    table = persist.init_run_db(db, run_id)
+    seen, items = set(), []
+    for r in rows:
+        if r['expr'] not in seen:
+            seen.add(r['expr'])
+            items.append((r['expr'], r['expr'], int(hashlib.sha256(r['expr'].encode()).hexdigest()[:12], 16),
+                          r.get('depth', 0)))
+    persist.insert_candidates(db, table, items)
+    rq = queue.Queue()
+    wt = threading.Thread(target=persist.result_writer, args=(run_id, table, db, rq), kwargs={'poll_s': 0.05})
+    wt.start()
+    n = validator_worker(run_id, table, db, 'force_free', None, rq, batch_size=64, idle_exit_s=1.0)
+    rq.put(None)
+    wt.join(timeout=60)
+    assert n == len(items)
+    rep = persist.report(db, table)
+    ok = {r['expr']: r['ok'] for r in rows}
+    assert rep['not_completed'] == 0
+    assert rep['valid'] == sum(ok[e] for e, *_ in items)
+    names = {name for _, name in rep['paper_solutions']}
+    assert {'Vertical field', 'X-point', 'Radial', 'Dipolar', 'Parabolic', 'Bent'} <= names, names
