@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, 'tests'))
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (spec; MI355X_MICROARCH.md lists FP32 157.3 = 2x)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s"
-DOMINANT = 'validate_kernel<0, double, 2, false>'   # pass 1 (force-free); Kerr: <1, ...>
+DOMINANT = 'grid_kernel<0>'   # pass 1 (force-free); Kerr: grid_kernel<1>
 
 
 def load_workload(problem):
@@ -108,7 +108,7 @@ def main():
     pid = PROBLEM_FORCE_FREE if a.problem == 'force_free' else PROBLEM_KERR
 
     slug = 'force_free' if pid == PROBLEM_FORCE_FREE else 'kerr_magnetosphere'
-    dominant = f'validate_kernel<{pid}, double, 2, false>'
+    dominant = f'grid_kernel<{pid}>'
     wname, ops_all, off_all, exprs_all = load_workload(slug)
     nprog = len(off_all) - 1
     total = a.n * world

@@ -197,7 +197,8 @@ int pdeval_pass_times(pdeval_ctx* ctx, float* ms, int max_passes, const char** n
  * [4] tier-2 stack 3, [5] tier-2 complex, [6] complex stack 8, [7] tier-2 stack 8,
  * [8] deep point pass (real, stack 3..8), [9] double-double point tier (real, stack <= 2),
  * [10] double-double point tier (complex), [11] double-double point tier (real, stack 3..8),
- * [12] complex tier 2, stack 5..8.                                                        */
+ * [12] complex tier 2, stack 5..8, [13] candidates the lean grid pass handed to the generic
+ * stack-2 kernel (malformed or point-stage-undecided programs; normally 0).              */
 int pdeval_pass_counts(pdeval_ctx* ctx, int64_t* counts, int max_counts);
 
 /* Diagnostics (force-free): one program at n_pts points (host arrays), tier-1 (tier2 = 0) or

@@ -19,6 +19,7 @@
 #include "pdeval_kernels.h"
 #include "pdeval_point.h"
 #include "pdeval_tier2.h"
+#include "pdeval_grid.h"
 #include "pdeval_launch.h"
 
 using namespace pd;
@@ -40,7 +41,8 @@ enum {
     L_DDC = 10,       // double-double point tier, complex
     L_DD8 = 11,       // double-double point tier, real, stack 3..8
     L_ESC_C_DEEP = 12,  // complex tier 2, stack 5..8
-    PD_N_LISTS = 13
+    L_SLOW = 13,      // lean grid pass -> the generic stack-2 kernel (malformed / undecided)
+    PD_N_LISTS = 14
 };
 
 struct pdeval_ctx {
@@ -527,8 +529,12 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 1: programs whose stack fits 2 jets (99 % of force-free depth 4), one wave per
     // candidate; deeper programs go to L_DEFER, tier-1 grid failures to L_ESC
     mark(2);
-    hipLaunchKernelGGL((validate_kernel<PROB, double, 2, false>), dim3((unsigned)blocks), dim3(256),
-                       (stack_lds<double, K, 2>(4)), s, a);
+    hipLaunchKernelGGL((grid_kernel<PROB>), dim3((unsigned)blocks), dim3(256), (stack_lds<double, K, 2>(4)), s, a,
+                       c->d_list[L_SLOW], cnt + L_SLOW);
+    HIPCHK(c, hipGetLastError());
+    // what the lean pass did not take (normally nothing): the generic kernel, same pass slot
+    hipLaunchKernelGGL((validate_kernel<PROB, double, 2, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
+                       dim3(64), (stack_lds<double, K, 2>(1)), s, follow(L_SLOW, L_DEFER, L_ESC));
     HIPCHK(c, hipGetLastError());
     // pass 2: stack 3 (2 LDS slots keep 10 waves per CU)
     mark(3);

@@ -538,11 +538,25 @@ template <class T, bool MAG> struct FFEpi {
 
 template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u, double rho) {
     PointResult r;
+#ifdef PD_VAR_NO_EPI   // timing variant: no determinant at all (verdicts meaningless)
+    {
+        r.res_abs = mag(u[1] * u[2]);
+        r.res_re = r.res_abs;
+        r.res_im = 0.0;
+        r.scale = 1.0;
+        r.grad_zero = false;
+        r.finite = true;
+        return r;
+    }
+#endif
     const T det = FFEpi<T, false>::eval(u, rho);
     // keep the signed and the magnitude evaluations apart: interleaved, the scheduler keeps
     // both sets of intermediates live
     __builtin_amdgcn_sched_barrier(0);
     double S;
+#ifdef PD_VAR_NO_MAG   // timing variant: no magnitude shadow (verdicts meaningless)
+    S = 1.0;
+#else
     if constexpr (Real<T>::cplx_pass) {
         double m[15];
 #pragma unroll
@@ -551,6 +565,7 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u
     } else {
         S = FFEpi<double, true>::eval(u, rho);
     }
+#endif
     r.res_abs = mag(det);
     if constexpr (Real<T>::cplx_pass) {
         r.res_re = ((const cplx*)&det)->re;
@@ -739,6 +754,15 @@ template <class T, int K, int MAXD> struct Interp {
                     break;
                 }
                 case PDOP_NEG:
+#ifdef PD_VAR_NEG_XOR   // sign flips as integer XORs of the high words (exact, like * -1)
+                    if constexpr (std::is_same<T, double>::value) {
+#pragma unroll
+                        for (int i = 0; i < NCJ; ++i)
+                            acc.c[i] = __hiloint2double(__double2hiint(acc.c[i]) ^ (int)0x80000000,
+                                                        __double2loint(acc.c[i]));
+                        break;
+                    }
+#endif
                     O::scale(acc, from_real<T>(-1.0));
                     break;
                 case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: {
