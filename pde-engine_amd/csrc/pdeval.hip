@@ -19,7 +19,6 @@
 #include "pdeval_kernels.h"
 #include "pdeval_point.h"
 #include "pdeval_tier2.h"
-#include "pdeval_grid.h"
 #include "pdeval_launch.h"
 
 using namespace pd;
@@ -529,8 +528,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 1: programs whose stack fits 2 jets (99 % of force-free depth 4), one wave per
     // candidate; deeper programs go to L_DEFER, tier-1 grid failures to L_ESC
     mark(2);
-    hipLaunchKernelGGL((grid_kernel<PROB>), dim3((unsigned)blocks), dim3(256), (stack_lds<double, K, 2>(4)), s, a,
-                       c->d_list[L_SLOW], cnt + L_SLOW);
+    launch_grid(PROB, (unsigned)blocks, stack_lds<double, K, 2>(4), s, a, c->d_list[L_SLOW], cnt + L_SLOW);
     HIPCHK(c, hipGetLastError());
     // what the lean pass did not take (normally nothing): the generic kernel, same pass slot
     hipLaunchKernelGGL((validate_kernel<PROB, double, 2, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),

@@ -1,6 +1,6 @@
-// pdeval_launch.h -- launchers of the rare point-stage kernels, compiled in their own
-// translation unit (pdeval_point.hip: the double-double and complex kernels are large, and a
-// separate unit builds in parallel with pdeval.hip).
+// pdeval_launch.h -- launchers of kernels compiled in their own translation units: the rare
+// point-stage kernels (pdeval_point.hip: the double-double and complex kernels are large) and
+// the lean grid pass (pdeval_grid.hip); separate units build in parallel with pdeval.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -16,4 +16,7 @@ void launch_dd_point(int problem, int kind, unsigned grid, hipStream_t s, const 
 // diagnostic: one program at the reference points in precision tier 0..3 (pdeval_point_eval)
 void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a, const int32_t* prog,
                        int plen, double* out, uint8_t* state);
+// the lean grid pass (pdeval_grid.hip): 256-thread blocks, 4 candidates each
+void launch_grid(int problem, unsigned blocks, size_t lds, hipStream_t s, const KernelArgs& a,
+                 int64_t* slow_list, int32_t* slow_count);
 }  // namespace pd
