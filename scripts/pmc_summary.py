@@ -21,7 +21,7 @@ def load(pass_dir):
     for f in files:
         for r in csv.DictReader(open(f)):
             k = r['Kernel_Name']
-            if 'validate_kernel' not in k:
+            if 'pd::' not in k:
                 continue
             k = k.split('(pd::')[0].replace('void pd::', '')
             agg[k][r['Counter_Name']] += float(r['Counter_Value'])

@@ -33,6 +33,7 @@ from gen_streams import make_scratch_copy  # noqa: E402
 
 _D = None      # GeneralFoliationDiscovery (reference) per worker
 _TIMEOUT = 60
+_FILTER_TIMEOUT = 120
 
 
 class _Timeout(BaseException):
@@ -94,10 +95,19 @@ def _filter_one(item):
         if sym is not None and d._has_degenerate_denominator(sym):
             out['degenerate'] = True
             return out
+        # the reference has no limit here; a fixture run bounds the dedupe key's simplify so
+        # one pathological candidate cannot stall the pool (such a row keeps its own string
+        # as key and is counted as 'simplify_timeout')
+        signal.alarm(_FILTER_TIMEOUT)
         try:
             out['normalized'] = str(sp.simplify(sp.expand(sym if sym is not None else sp.sympify(s))))
+        except _Timeout:
+            out['normalized'] = s
+            out['simplify_timeout'] = True
         except Exception:
             out['normalized'] = s
+        finally:
+            signal.alarm(0)
         syms = d.problem.symbols
         uc = u if u is not None else sp.sympify(s, locals=d._sympify_locals)
         if not (uc.has(syms.get('rho', sp.Symbol('rho'))) or uc.has(syms.get('z', sp.Symbol('z')))
@@ -159,9 +169,15 @@ def main():
     if a.mode == 'filters':
         items = read_stream(a.input)
         with mp.get_context('fork').Pool(a.procs, _init_worker, (a.ref, a.problem)) as pool:
-            res = pool.map(_filter_one, items, chunksize=16)
-        seen, kept, stats = set(), [], {'degenerate': 0, 'duplicate': 0, 'const_only': 0}
+            res = []
+            for r in pool.imap(_filter_one, items, chunksize=16):
+                res.append(r)
+                if len(res) % 10000 == 0:
+                    print(f'[filters] {len(res)}/{len(items)} {time.time()-t0:.0f}s', flush=True)
+        seen, kept, stats = set(), [], {'degenerate': 0, 'duplicate': 0, 'const_only': 0,
+                                        'simplify_timeout': 0}
         for r in res:                       # sequential, stream order (UNIQUE(normalized))
+            stats['simplify_timeout'] += int(bool(r.get('simplify_timeout')))
             if r['degenerate']:
                 stats['degenerate'] += 1
                 continue
