@@ -193,6 +193,7 @@ typedef struct {
     int finite, grad_zero;
     double u0;
     double noise;   /* tier 2 only: first-order rounding-noise bound of the residual */
+    double grad[2], grad_err[2];   /* quad tier: |u_x|, |u_y| and their error bounds (EPSQ units) */
 } pt_result;
 
 /* gamma for the finite-difference form of the first-order noise bound: the noise is
@@ -303,6 +304,10 @@ static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, 
     r.res_re = (double)crealq(res);
     r.finite = fin && finiteq(crealq(res)) && finiteq(cimagq(res)) && isfinite(r.scale) && isfinite(r.noise);
     r.grad_zero = cq[IDX(1, 0)] == 0 && cq[IDX(0, 1)] == 0;
+    r.grad[0] = (double)cabsq(cq[IDX(1, 0)]);
+    r.grad[1] = (double)cabsq(cq[IDX(0, 1)]);
+    r.grad_err[0] = W[IDX(1, 0)];
+    r.grad_err[1] = W[IDX(0, 1)];
     r.u0 = (double)crealq(cq[0]);
     return r;
 }
@@ -325,7 +330,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
         int64_t nw = offsets[ci + 1] - offsets[ci];
         int cls = -1, cplx = 0;
         double qr = 0, qmax = 0;
-        int nb = 0, nnf = 0, nfin = 0, any_grad = 0, point_reject = 0;
+        int nb = 0, nnf = 0, nfin = 0, any_grad = 0, point_reject = 0, gconst = 1;
         if (nw < 2 || (w[0] & 0xff) != 0) cls = PDEVAL_CLS_BAD_PROGRAM;
         const uint32_t hdr = nw > 0 ? (uint32_t)w[0] : 0u;
         if (cls < 0 && (hdr & PDEVAL_FLAG_COMPLEX)) {
@@ -333,7 +338,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
             else cls = PDEVAL_CLS_REJECT_POINT;                   /* Kerr: non-real at a test point */
         }
     again:
-        qr = 0; qmax = 0; nb = nnf = nfin = any_grad = point_reject = 0;
+        qr = 0; qmax = 0; nb = nnf = nfin = any_grad = point_reject = 0; gconst = 1;
         for (int p = 0; p < npts && cls < 0; ++p) {
             int rc;
             pt_result r = eval_point(problem, w, nw, px[p], py[p], cplx, 0, &rc);
@@ -353,6 +358,11 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                 if (rcq) { cls = PDEVAL_CLS_BAD_PROGRAM; break; }
                 /* a complex residual is reported as its modulus with the sign of its real part */
                 if (res_ref) res_ref[ci * nref + p] = copysign(q.res_abs, q.res_re);
+                /* Kerr constant exclusion (kerr validator.py:231-240: simplify(u) has neither r
+                 * nor x): at every reference point the gradient is within its rounding bound */
+                gconst = gconst && q.finite &&
+                         q.grad[0] <= prm->noise_kappa * (double)EPSQ * q.grad_err[0] &&
+                         q.grad[1] <= prm->noise_kappa * (double)EPSQ * q.grad_err[1];
                 if (!q.finite) {
                     if (problem == PDEVAL_PROBLEM_FORCE_FREE && !cplx) { cplx = 1; goto again; }
                     point_reject = 1;    /* non-finite at a reference point: final */
@@ -391,6 +401,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
         }
         if (cls < 0) {
             int structural = problem != PDEVAL_PROBLEM_FORCE_FREE || (hdr & PDEVAL_FLAG_NOCOORD);
+            if (problem != PDEVAL_PROBLEM_FORCE_FREE && gconst) any_grad = 0;
             if (!any_grad && nfin > 0 && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
             else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;
             else if (nb > prm->max_bad) cls = PDEVAL_CLS_REJECT_GRID;

@@ -41,7 +41,8 @@ enum {
     L_DD8 = 11,       // double-double point tier, real, stack 3..8
     L_ESC_C_DEEP = 12,  // complex tier 2, stack 5..8
     L_SLOW = 13,      // lean grid pass -> the generic stack-2 kernel (malformed / undecided)
-    PD_N_LISTS = 14
+    L_SLOW2 = 14,     // lean stack-3 pass -> the generic stack-3 kernel
+    PD_N_LISTS = 15
 };
 
 struct pdeval_ctx {
@@ -278,8 +279,8 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
 
 extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (!c) return PDEVAL_ERR_ARG;
-    hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) pdeval_comm_destroy(c);
     for (int64_t* l : c->d_list)
         if (l) (void)hipFree(l);
@@ -288,10 +289,10 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->d_noise) (void)hipFree(c->d_noise);
     for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
     for (hipEvent_t& e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PDEVAL_OK;
 }
@@ -528,16 +529,19 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 1: programs whose stack fits 2 jets (99 % of force-free depth 4), one wave per
     // candidate; deeper programs go to L_DEFER, tier-1 grid failures to L_ESC
     mark(2);
-    launch_grid(PROB, (unsigned)blocks, stack_lds<double, K, 2>(4), s, a, c->d_list[L_SLOW], cnt + L_SLOW);
+    launch_grid(PROB, (unsigned)blocks, s, a, c->d_list[L_SLOW], cnt + L_SLOW);
     HIPCHK(c, hipGetLastError());
     // what the lean pass did not take (normally nothing): the generic kernel, same pass slot
     hipLaunchKernelGGL((validate_kernel<PROB, double, 2, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
                        dim3(64), (stack_lds<double, K, 2>(1)), s, follow(L_SLOW, L_DEFER, L_ESC));
     HIPCHK(c, hipGetLastError());
-    // pass 2: stack 3 (2 LDS slots keep 10 waves per CU)
+    // pass 2: stack 3, the lean interpreter over the L_DEFER list (64-thread blocks, 2 LDS
+    // slots); what it does not take, the generic stack-3 kernel
     mark(3);
-    hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3(pgrid), dim3(64),
-                       (stack_lds<double, K, 3>(1)), s, follow(L_DEFER, L_DEFER2, L_ESC));
+    launch_grid_list(PROB, pgrid, s, follow(L_DEFER, L_DEFER2, L_ESC), c->d_list[L_SLOW2], cnt + L_SLOW2);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
+                       dim3(64), (stack_lds<double, K, 3>(1)), s, follow(L_SLOW2, L_DEFER2, L_ESC));
     HIPCHK(c, hipGetLastError());
     // pass 3: stack 4..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
     mark(4);
@@ -673,14 +677,14 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
     }
     HIPCHK(c, hipSetDevice(c->device));
     if (n_words > c->hcap_words) {
-        if (c->d_ops) hipFree(c->d_ops);
+        if (c->d_ops) (void)hipFree(c->d_ops);
         c->d_ops = nullptr;
         c->hcap_words = 0;
         HIPCHK(c, hipMalloc(&c->d_ops, n_words * sizeof(int32_t)));
         c->hcap_words = n_words;
     }
     if (n + 1 > c->hcap_n) {
-        if (c->d_off) hipFree(c->d_off);
+        if (c->d_off) (void)hipFree(c->d_off);
         c->d_off = nullptr;
         c->hcap_n = 0;
         HIPCHK(c, hipMalloc(&c->d_off, (n + 1) * sizeof(int64_t)));
@@ -691,7 +695,7 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
     const int64_t sz_bits = (nb + 15) / 16 * 16, sz_st = (n + 15) / 16 * 16;
     const int64_t need = sz_bits + sz_st + 8 * n * (3 + c->n_ref + PDEVAL_FP_N) + 8 * n * 2;
     if (need > c->outbuf_bytes) {
-        if (c->d_outbuf) hipFree(c->d_outbuf);
+        if (c->d_outbuf) (void)hipFree(c->d_outbuf);
         c->d_outbuf = nullptr;
         c->outbuf_bytes = 0;
         HIPCHK(c, hipMalloc(&c->d_outbuf, need));

@@ -49,8 +49,8 @@ constexpr uint64_t kPOpMask = op_bit(PDOP_ADD_P) | op_bit(PDOP_SUB_P) | op_bit(P
 constexpr uint64_t kVarMask = op_bit(PDOP_MUL_X) | op_bit(PDOP_MUL_Y) | op_bit(PDOP_DIV_X) |
                               op_bit(PDOP_DIV_Y);
 
-// Program words [1, plen) run by Lean::run with a 2-jet stack?  Wave-uniform, scalar only.
-__device__ __forceinline__ bool lean_prescan(const int32_t* prog, int plen) {
+// Program words [1, plen) run by Lean::run with a MAXD-jet stack?  Wave-uniform, scalar only.
+template <int MAXD> __device__ __forceinline__ bool lean_prescan(const int32_t* prog, int plen) {
     if (plen < 2) return false;
     int pc = 1, d = 0;
     while (pc < plen) {
@@ -61,7 +61,7 @@ __device__ __forceinline__ bool lean_prescan(const int32_t* prog, int plen) {
         const int len = (kImmMask & b) ? ((w & PDEVAL_IMM_DD) ? 5 : 3) : 1;
         if (pc + len > plen) return false;
         if (kPushMask & b) {
-            if (++d > 2) return false;
+            if (++d > MAXD) return false;
         } else if (kBinMask & b) {
             if (d < 2) return false;
             --d;
@@ -75,27 +75,40 @@ __device__ __forceinline__ bool lean_prescan(const int32_t* prog, int plen) {
     return d == 1;
 }
 
-template <int K> struct Lean {
+// W sample points per lane (W grid rows per dispatch of one opcode): the opcode decode, the
+// dispatch branches and the immediate loads are paid once for W jets.  Force-free runs W = 1
+// (two 15-coefficient jets per operand would not fit 128 VGPRs); Kerr's 6-coefficient jets run
+// W = 2.  For every point the arithmetic is the same JetOps sequence as at W = 1.
+template <int K, int W, int MAXD> struct Lean {
     using O = JetOps<double, K>;
     using J = typename O::J;
     static constexpr int NCJ = nc(K);
 
-    static __device__ __forceinline__ void store(double* stk, int lane, const J& t) {
+    static constexpr int SLOT = W * NCJ * 64;   // doubles per operand slot
+
+    // LDS operand slot of one wave: [w][coef][lane]
+    static __device__ __forceinline__ void store(double* stk, int lane, const J (&t)[W]) {
 #pragma unroll
-        for (int c = 0; c < NCJ; ++c) stk[c * 64 + lane] = t.c[c];
+        for (int w = 0; w < W; ++w)
+#pragma unroll
+            for (int c = 0; c < NCJ; ++c) stk[(w * NCJ + c) * 64 + lane] = t[w].c[c];
     }
-    static __device__ __forceinline__ void load(const double* stk, int lane, J& t) {
+    static __device__ __forceinline__ void load(const double* stk, int lane, J (&t)[W]) {
 #pragma unroll
-        for (int c = 0; c < NCJ; ++c) t.c[c] = stk[c * 64 + lane];
+        for (int w = 0; w < W; ++w)
+#pragma unroll
+            for (int c = 0; c < NCJ; ++c) t[w].c[c] = stk[(w * NCJ + c) * 64 + lane];
     }
 
-    // Evaluate a prescanned program at (x, y); inv_x = 1/x, inv_y = 1/y (as rcp() forms them).
-    static __device__ __forceinline__ void run(const int32_t* prog, int plen, double x, double y,
-                                               double inv_x, double inv_y, J& acc, double* stk,
-                                               int lane) {
+    // Evaluate a prescanned program at (x[w], y), w < W; inv_x = 1/x, inv_y = 1/y (as rcp()
+    // forms them).  x[] is wave-uniform (one grid row each), y is the lane's ordinate.
+    static __device__ __forceinline__ void run(const int32_t* prog, int plen, const double (&x)[W], double y,
+                                               const double (&inv_x)[W], double inv_y, J (&acc)[W],
+                                               double* stk, int lane) {
         int pc = 1;
         uint32_t w = rd_word(prog + 1);
         bool first = true;
+        int d = 0;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
         for (;;) {
             const uint32_t op = w & 0xffu;
             const bool has_imm = (kImmMask >> op) & 1u;
@@ -111,74 +124,114 @@ template <int K> struct Lean {
             // unstructured joins the structurizer turns into extra flow masks and copies
             const uint64_t b = 1ull << op;
             if (b & kPushMask) {
-                if (!first) store(stk, lane, acc);
+                if (!first) store(stk + (MAXD == 2 ? 0 : d - 1) * SLOT, lane, acc);
+                ++d;
                 if (op == PDOP_PUSH_X) {
-                    O::set_var(acc, x, 0);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::set_var(acc[q], x[q], 0);
                 } else if (op == PDOP_PUSH_P) {
                     double pk[K + 1];
                     if (on_y) {
                         O::pcoefs(y, pn, pk);
-                        O::template set_p<1>(acc, pk);
+#pragma unroll
+                        for (int q = 0; q < W; ++q) O::template set_p<1>(acc[q], pk);
                     } else {
-                        O::pcoefs(x, pn, pk);
-                        O::template set_p<0>(acc, pk);
+#pragma unroll
+                        for (int q = 0; q < W; ++q) {
+                            O::pcoefs(x[q], pn, pk);
+                            O::template set_p<0>(acc[q], pk);
+                        }
                     }
                 } else if (op == PDOP_PUSH_Y) {
-                    O::set_var(acc, y, 1);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
                 } else {
-                    O::set_const(acc, rd_imm(prog + pc + 1));
+                    const double c = rd_imm(prog + pc + 1);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::set_const(acc[q], c);
                 }
             } else if (b & kCheapMask) {
                 if (op == PDOP_ADDC) {
-                    acc.c[0] = acc.c[0] + rd_imm(prog + pc + 1);
+                    const double c = rd_imm(prog + pc + 1);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
                 } else if (op == PDOP_NEG) {
-                    O::scale(acc, -1.0);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::scale(acc[q], -1.0);
                 } else if (op == PDOP_MULC) {
-                    O::scale(acc, rd_imm(prog + pc + 1));
+                    const double c = rd_imm(prog + pc + 1);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::scale(acc[q], c);
                 } else if (op == PDOP_ADD_X) {
-                    acc.c[0] = acc.c[0] + x;
-                    acc.c[ji(1, 0)] = acc.c[ji(1, 0)] + 1.0;
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        acc[q].c[0] = acc[q].c[0] + x[q];
+                        acc[q].c[ji(1, 0)] = acc[q].c[ji(1, 0)] + 1.0;
+                    }
                 } else if (op == PDOP_SUB_X) {
-                    acc.c[0] = acc.c[0] + (-x);
-                    acc.c[ji(1, 0)] = acc.c[ji(1, 0)] + (-1.0);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        acc[q].c[0] = acc[q].c[0] + (-x[q]);
+                        acc[q].c[ji(1, 0)] = acc[q].c[ji(1, 0)] + (-1.0);
+                    }
                 } else if (op == PDOP_ADD_Y) {
-                    acc.c[0] = acc.c[0] + y;
-                    acc.c[ji(0, 1)] = acc.c[ji(0, 1)] + 1.0;
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        acc[q].c[0] = acc[q].c[0] + y;
+                        acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + 1.0;
+                    }
                 } else {
-                    acc.c[0] = acc.c[0] + (-y);
-                    acc.c[ji(0, 1)] = acc.c[ji(0, 1)] + (-1.0);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        acc[q].c[0] = acc[q].c[0] + (-y);
+                        acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + (-1.0);
+                    }
                 }
             } else if (b & kPOpMask) {
                 double pk[K + 1];
                 if (on_y) {
                     O::pcoefs(y, pn, pk);
-                    O::template p_op<1>(op, acc, pk);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::template p_op<1>(op, acc[q], pk);
                 } else {
-                    O::pcoefs(x, pn, pk);
-                    O::template p_op<0>(op, acc, pk);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        O::pcoefs(x[q], pn, pk);
+                        O::template p_op<0>(op, acc[q], pk);
+                    }
                 }
             } else if (b & kBinMask) {
-                J l;
-                load(stk, lane, l);
-                if (op == PDOP_DIV) O::div(l, acc);
-                else if (op == PDOP_SUB) O::sub(l, acc);
-                else if (op == PDOP_ADD) O::add(l, acc);
-                else if (op == PDOP_MUL) O::mul(l, acc);
-                else if (op == PDOP_RDIV) O::rdiv(l, acc);
-                else O::rsub(l, acc);
+                J l[W];
+                load(stk + (MAXD == 2 ? 0 : d - 2) * SLOT, lane, l);
+                --d;
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    if (op == PDOP_DIV) O::div(l[q], acc[q]);
+                    else if (op == PDOP_SUB) O::sub(l[q], acc[q]);
+                    else if (op == PDOP_ADD) O::add(l[q], acc[q]);
+                    else if (op == PDOP_MUL) O::mul(l[q], acc[q]);
+                    else if (op == PDOP_RDIV) O::rdiv(l[q], acc[q]);
+                    else O::rsub(l[q], acc[q]);
+                }
             } else if (b & kVarMask) {
-                if (op == PDOP_DIV_Y) div_var(acc, y, inv_y, 1);
-                else if (op == PDOP_MUL_X) O::mul_var(acc, x, 0);
-                else if (op == PDOP_DIV_X) div_var(acc, x, inv_x, 0);
-                else O::mul_var(acc, y, 1);
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    if (op == PDOP_DIV_Y) div_var(acc[q], y, inv_y, 1);
+                    else if (op == PDOP_MUL_X) O::mul_var(acc[q], x[q], 0);
+                    else if (op == PDOP_DIV_X) div_var(acc[q], x[q], inv_x[q], 0);
+                    else O::mul_var(acc[q], y, 1);
+                }
             } else {
-                if (op == PDOP_EXP) O::expj(acc);
-                else if (op == PDOP_POW) O::powa(acc, rd_imm(prog + pc + 1));
-                else if (op == PDOP_RDIVC) O::rdivc(acc, rd_imm(prog + pc + 1));
-                else if (op == PDOP_SQRT) O::sqrtj(acc);
-                else if (op == PDOP_LOG) O::logj(acc);
-                else if (op == PDOP_POWN) O::pown(acc, pn);
-                else absj<K>(acc);
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+                    if (op == PDOP_EXP) O::expj(acc[q]);
+                    else if (op == PDOP_POW) O::powa(acc[q], rd_imm(prog + pc + 1));
+                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], rd_imm(prog + pc + 1));
+                    else if (op == PDOP_SQRT) O::sqrtj(acc[q]);
+                    else if (op == PDOP_LOG) O::logj(acc[q]);
+                    else if (op == PDOP_POWN) O::pown(acc[q], pn);
+                    else absj<K>(acc[q]);
+                }
             }
             if (!more) break;
             first = false;
@@ -240,24 +293,38 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 #ifndef PD_GRID_WAVES_PER_SIMD
 #define PD_GRID_WAVES_PER_SIMD 4
 #endif
-// One wave per candidate, 4 per 256-thread block; a.defer_list takes stack-3+ programs (pass 2),
-// a.slow_list what the lean path does not take (drained by the generic kernel).
-template <int PROB>
-__global__ __launch_bounds__(256, PD_GRID_WAVES_PER_SIMD) void grid_kernel(KernelArgs a, int64_t* slow_list,
-                                                                          int32_t* slow_count) {
-    constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
-    using L = Lean<K>;
-    using J = typename L::J;
-    const int lane = threadIdx.x & 63;
-    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifndef PD_HOST_SIM
-    extern __shared__ __align__(16) unsigned char pd_lds[];
-#else
-    static unsigned char pd_lds[1];
+#ifndef PD_KERR_W
+#define PD_KERR_W 2
 #endif
-    double* stk = reinterpret_cast<double*>(pd_lds) + (size_t)wib * nc(K) * 64;
-    const int64_t cand = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
-    if (cand >= a.n) return;
+#ifndef PD_DEEP_W
+#define PD_DEEP_W 2
+#endif
+// Two lean passes share one body (grid_body):
+//   pass 1  grid_kernel       every candidate, one wave each (256-thread blocks), stack <= 2
+//                             (one LDS operand slot); deeper programs -> a.defer_list
+//   pass 2  grid_list_kernel  persistent over the stack-3 list (64-thread blocks, two slots);
+//                             deeper -> a.defer_list (the generic stack-8 pass)
+// Folding stack 3 into pass 1 (a runtime slot index, and two slots of LDS per wave for every
+// candidate) measured slower for Kerr: 66.1 ms against 49.9 + 13.5 ms (d<=3 batch).
+// W = grid rows per dispatch (Lean above): 1 for force-free, PD_KERR_W for Kerr in pass 1,
+// PD_DEEP_W for Kerr in pass 2; an odd last row runs alone.
+template <int PROB, int MAXD> constexpr int grid_w() {
+    return PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : (MAXD == 2 ? PD_KERR_W : PD_DEEP_W);
+}
+template <int PROB> constexpr int grid_k() { return PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2; }
+// dynamic LDS of one block of `waves` waves: (MAXD - 1) operand slots of W jets each
+template <int PROB, int MAXD> constexpr size_t grid_lds(int waves) {
+    return (size_t)waves * (MAXD - 1) * grid_w<PROB, MAXD>() * nc(grid_k<PROB>()) * 64 * sizeof(double);
+}
+
+// The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots.
+template <int PROB, int MAXD>
+__device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int lane, double* stk,
+                                          int64_t* slow_list, int32_t* slow_count) {
+    constexpr int K = grid_k<PROB>();
+    constexpr int W = grid_w<PROB, MAXD>();
+    using L = Lean<K, W, MAXD>;
+    using J = typename L::J;
     const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
     const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24);
     const int32_t* prog = a.ops + (in_bounds ? beg : 0);
@@ -267,11 +334,11 @@ __global__ __launch_bounds__(256, PD_GRID_WAVES_PER_SIMD) void grid_kernel(Kerne
     if (ps & P0_CPLX) return;                                    // the complex passes take it
     if ((ps & 3) == P0_REJECT && !a.prm.full_grid) return;      // final after the point stage
     bool slow = !in_bounds || (hdr & 0xffu) != 0u || (ps & 3) == P0_NONE || (hdr & PDEVAL_FLAG_COMPLEX);
-    if (!slow && (int)((hdr >> 8) & 0xffu) > 2) {
+    if (!slow && (int)((hdr >> 8) & 0xffu) > MAXD) {
         if (lane == 0) list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
         return;
     }
-    if (!slow) slow = !lean_prescan(prog, plen);
+    if (!slow) slow = !lean_prescan<MAXD>(prog, plen);
     if (slow) {
         if (lane == 0) list_append(slow_list, slow_count, a.list_capacity, cand);
         return;
@@ -282,38 +349,91 @@ __global__ __launch_bounds__(256, PD_GRID_WAVES_PER_SIMD) void grid_kernel(Kerne
     double qmax = 0.0;
     int nbad = 0, nfin = 0;
     bool grad_nz = (ps & P0_GRAD) != 0;
-    for (int row = 0; row < a.nx; ++row) {
-        const double x = rd_sf64(a.gx + row);
-        const double inv_x = rcp(x);
+    for (int row = 0; row < a.nx; row += W) {
+        double x[W], inv_x[W];
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            x[q] = rd_sf64(a.gx + min(row + q, a.nx - 1));   // a tail row past nx: unused
+            inv_x[q] = rcp(x[q]);
+        }
         for (int sl = 0; sl < per_row; ++sl) {
             const double y = per_row == 1 ? y0 : a.gy[sl * 64 + lane];
             const double inv_y = per_row == 1 ? inv_y0 : rcp(y);
-            const int base = a.n_ref + row * a.ny + sl * 64;   // point index of lane 0
-            J u;
-            L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane);
-            PointResult r;
-            if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);
-            else r = kerr_epilogue<double>(u.c, a.kc + 4 * (base + lane));
-            const double qv = scaled(r.res_abs, r.scale);
-            if (a.out.fingerprint) {
+            // Kerr: this point's operator coefficients (a 128 KiB table, L2-resident) are loaded
+            // before the program runs, so their latency hides under the interpreter
+            double kv[W][4];
+            if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
 #pragma unroll
-                for (int f = 0; f < PDEVAL_FP_N; ++f) {
-                    const int rel = a.fp_pts[f] - base;   // uniform
-                    if (rel >= 0 && rel < 64 && lane == rel) a.out.fingerprint[cand * PDEVAL_FP_N + f] = u.c[0];
+                for (int q = 0; q < W; ++q) {
+                    const double* kp = a.kc + 4 * (a.n_ref + min(row + q, a.nx - 1) * a.ny + sl * 64 + lane);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) kv[q][i] = kp[i];
                 }
             }
-            if (r.finite) {
-                qmax = fmax(qmax, qv);
-                if (!r.grad_zero) grad_nz = true;
+            J u[W];
+            L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane);
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                if (W > 1 && row + q >= a.nx) break;                     // uniform
+                const int base = a.n_ref + (row + q) * a.ny + sl * 64;   // point index of lane 0
+                PointResult r;
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u[q].c, x[q]);
+                else r = kerr_epilogue<double>(u[q].c, kv[q]);
+                const double qv = scaled(r.res_abs, r.scale);
+                if (a.out.fingerprint) {
+#pragma unroll
+                    for (int f = 0; f < PDEVAL_FP_N; ++f) {
+                        const int rel = a.fp_pts[f] - base;   // uniform
+                        if (rel >= 0 && rel < 64 && lane == rel) a.out.fingerprint[cand * PDEVAL_FP_N + f] = u[q].c[0];
+                    }
+                }
+                if (r.finite) {
+                    qmax = fmax(qmax, qv);
+                    if (!r.grad_zero) grad_nz = true;
+                }
+                nfin += (int)__popcll(__ballot(r.finite));
+                nbad += (int)__popcll(__ballot(r.finite && qv > a.prm.tau_grid));
             }
-            nfin += (int)__popcll(__ballot(r.finite));
-            nbad += (int)__popcll(__ballot(r.finite && qv > a.prm.tau_grid));
         }
     }
     qmax = wave_max(qmax);
-    const bool any_grad = __any(grad_nz);
+    const bool any_grad = __any(grad_nz) && !(ps & P0_CONST);
     if (lane == 0)
         grid_finish(a, cand, hdr, PROB, (ps & 3) == P0_REJECT, qmax, nbad, nfin, a.nx * a.ny - nfin, any_grad);
+}
+
+// pass 1: one wave per candidate, 4 per 256-thread block; a.defer_list takes stack-3+ programs,
+// slow_list what the lean path does not take (drained by the generic kernel)
+template <int PROB>
+__global__ __launch_bounds__(256, PD_GRID_WAVES_PER_SIMD) void grid_kernel(KernelArgs a, int64_t* slow_list,
+                                                                          int32_t* slow_count) {
+#ifndef PD_HOST_SIM
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
+    const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    double* stk = reinterpret_cast<double*>(pd_lds) + (size_t)wib * grid_lds<PROB, 2>(1) / sizeof(double);
+    const int64_t cand = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
+    if (cand >= a.n) return;
+    grid_body<PROB, 2>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
+}
+
+// pass 2: the stack-3 list a.list (count *a.list_count), persistent 64-thread blocks
+template <int PROB>
+__global__ __launch_bounds__(64) void grid_list_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
+#ifndef PD_HOST_SIM
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
+    double* stk = reinterpret_cast<double*>(pd_lds);
+    int64_t nwork = (int64_t)(*a.list_count);
+    if (nwork > a.list_capacity) nwork = a.list_capacity;
+    for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+        const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
+        grid_body<PROB, 3>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
+    }
 }
 
 }  // namespace pd

@@ -7,14 +7,24 @@
 
 namespace pd {
 
-void launch_grid(int problem, unsigned blocks, size_t lds, hipStream_t s, const KernelArgs& a,
+void launch_grid(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
                  int64_t* slow_list, int32_t* slow_count) {
     if (problem == PDEVAL_PROBLEM_FORCE_FREE)
-        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(256), lds, s, a,
-                           slow_list, slow_count);
+        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(256),
+                           (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2>(4)), s, a, slow_list, slow_count);
     else
-        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(256), lds, s, a, slow_list,
-                           slow_count);
+        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(256),
+                           (grid_lds<PDEVAL_PROBLEM_KERR, 2>(4)), s, a, slow_list, slow_count);
+}
+
+void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
+                      int64_t* slow_list, int32_t* slow_count) {
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE)
+        hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(64),
+                           (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 3>(1)), s, a, slow_list, slow_count);
+    else
+        hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(64),
+                           (grid_lds<PDEVAL_PROBLEM_KERR, 3>(1)), s, a, slow_list, slow_count);
 }
 
 }  // namespace pd

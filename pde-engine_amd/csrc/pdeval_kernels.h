@@ -73,8 +73,11 @@ enum : uint32_t {
 //   P0_GRAD  a reference point has a non-zero gradient
 //   P0_DD    undecided in fp64 (value too close to its noise or to a threshold): treated as
 //            PASS by the grid passes, decided by the double-double tier at the end
+//   P0_CONST (Kerr) u is constant: at every reference point its gradient lies within the
+//            error bound of its rounding (kerr validator.py:231-240 drops u when simplify(u) has
+//            neither r nor x; a constant's computed gradient is rounding noise, never exactly 0)
 enum : uint8_t { P0_NONE = 0, P0_PASS = 1, P0_REJECT = 2, P0_CPLX = 4, P0_PROV = 8, P0_GRAD = 16,
-                 P0_DD = 32 };
+                 P0_DD = 32, P0_CONST = 64 };
 
 #define PD_ESC_SHIFT 48
 #define PD_ESC_CAND_MASK ((1ll << PD_ESC_SHIFT) - 1)
@@ -853,13 +856,16 @@ void validate_kernel(KernelArgs a) {
         if ((ps & 3) == P0_REJECT && !a.prm.full_grid) continue;  // final after the point stage
         const bool p0 = (ps & 3) != P0_NONE;
         if constexpr (!Real<T>::cplx_pass) {
-            if (status < 0 && !p0 && (hdr & PDEVAL_FLAG_COMPLEX)) {
+            if (status < 0 && (hdr & PDEVAL_FLAG_COMPLEX)) {
                 if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
                     // complex-valued program: straight to the complex pass
-                    if (lane == 0 && a.cplx_list) list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
-                    status = PDEVAL_CLS_NONFINITE_REF;
+                    if (!p0) {
+                        if (lane == 0 && a.cplx_list) list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
+                        status = PDEVAL_CLS_NONFINITE_REF;
+                    }
                 } else {
-                    // Kerr: a non-real value at a test point rejects (kerr validator.py:179-180)
+                    // Kerr: a non-real value at a test point rejects (kerr validator.py:179-180),
+                    // final whether or not pass 0 saw it first: the real grid cannot evaluate it
                     status = PDEVAL_CLS_REJECT_POINT;
                 }
             }
@@ -969,7 +975,7 @@ void validate_kernel(KernelArgs a) {
         }
         // wave reductions
         qmax = wave_max(qmax);
-        const bool any_grad = __any(grad_nz);
+        const bool any_grad = __any(grad_nz) && !(ps & P0_CONST);
         if (lane == 0) {
             int cls = status;
             if (cls < 0) {

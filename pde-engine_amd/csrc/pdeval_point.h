@@ -55,6 +55,7 @@ struct PtEval {
     double S, noise;                 // magnitude scale and first-order noise bound
     double u0;                       // Re u at the point (fingerprint)
     bool finite, grad_zero;
+    bool grad_noise;                 // |u_x|, |u_y| within kappa x their rounding-error bounds
     int rc;                          // RUN_*
 };
 
@@ -103,6 +104,9 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
     r.res_abs = mag(res);
     r.u0 = re_hi(u.c[0]);
     r.grad_zero = is_zero(u.c[ji(1, 0)]) && is_zero(u.c[ji(0, 1)]);
+    // coefficient i is within eps * e[i] of exact (first order; dd: dd_unit * e[i])
+    const double gk = a.prm.noise_kappa * kEps * unit;
+    r.grad_noise = m[ji(1, 0)] <= gk * e[ji(1, 0)] && m[ji(0, 1)] <= gk * e[ji(0, 1)];
     bool fin = finite_(res) && isfinite(r.S) && isfinite(r.noise);
 #pragma unroll
     for (int i = 0; i < NC; ++i) fin = fin && m[i] < kHugeJet;
@@ -148,7 +152,7 @@ template <int PROB, class T, class V, int MAXD, bool VEC, bool FINAL, class STK>
 __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand, const int32_t* prog, int plen,
                                                uint32_t hdr, STK& stk, bool* nonfinite, bool* prog_err) {
     double qr = 0.0;
-    bool nf = false, grad = false, rej = false, und = false, inacc = false;
+    bool nf = false, grad = false, rej = false, und = false, inacc = false, gconst = true;
     uint8_t ff = P0_PASS;
     *prog_err = false;
     for (int p = 0; p < a.n_ref; ++p) {
@@ -162,6 +166,7 @@ __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand
         if (!FINAL && a.noise_ref) a.noise_ref[cand * a.n_ref + p] = r.noise;
         // (a complex residual: its modulus with the sign of its real part)
         if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = r.res_im == 0.0 ? r.res_re : copysign(r.res_abs, r.res_re);
+        gconst = gconst && r.finite && r.grad_noise;
         if (!r.finite) {
             nf = true;
             // finite, but a coefficient beyond the 2^160 guard: a sure reject whose value the
@@ -189,6 +194,7 @@ __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand
     else ps = und ? (uint8_t)(P0_DD | P0_PASS) : (rej ? P0_REJECT : P0_PASS);
     if (inacc) ps |= P0_DD;
     if (grad) ps |= P0_GRAD;
+    if (PROB != PDEVAL_PROBLEM_FORCE_FREE && gconst) ps |= P0_CONST;
     return ps;
 }
 

@@ -533,7 +533,9 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             qmax = wave_max(qmax);
             nbad_out = nb1 <= a.prm.max_bad ? nb1 : nb2;
         }
-        const bool any_grad = __any(grad_nz) || (flags & ESC_ANY_GRAD);
+        // (P0_CONST: a Kerr constant whose gradient is rounding noise -- pdeval_kernels.h)
+        const bool pconst = a.pstate && (a.pstate[cand] & P0_CONST);
+        const bool any_grad = (__any(grad_nz) || (flags & ESC_ANY_GRAD)) && !pconst;
         if (lane == 0) {
             const bool has_fin = eval_grid ? nfin > 0 : (flags & ESC_NFIN) != 0;
             const bool structural = (PROB != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);

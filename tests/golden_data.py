@@ -26,7 +26,15 @@ def stream(name, with_index=False):
 
 
 FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl')
-KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl')
+KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl', 'kerr_d4_s2000.jsonl',
+            'kerr_d4_accepts.jsonl')
+# Kerr candidates whose reason class differs from the reference's, with the same verdict: the
+# device and the oracle substitute M = 1, a = 1/10 before validating (the reference's point
+# check values), while the reference's constant test and symbolic stage keep M and a symbolic
+# (kerr validator.py:231-240, :279-300).  This u is constant only at M = 1: here "Trivial
+# constant solution excluded", there "PDE residual != 0".  (1 of the 1,024,799
+# candidates of the Kerr depth<=4 stream.)
+KERR_PARAM_CLASS = {'exp(a**2)*exp(2*r)*exp(-2*M*r)'}
 
 
 def exact_rows(name='ff_d4_exact_det.jsonl'):
