@@ -60,6 +60,8 @@ template <int MAXD> __device__ __forceinline__ bool lean_prescan(const int32_t* 
         const uint64_t b = 1ull << op;
         const int len = (kImmMask & b) ? ((w & PDEVAL_IMM_DD) ? 5 : 3) : 1;
         if (pc + len > plen) return false;
+        // POWN beyond 8 takes the generic kernel (see pown_lean; none in the depth-4 streams)
+        if (op == PDOP_POWN && ((w >> 8) & 0xffu) > 8u) return false;
         if (kPushMask & b) {
             if (++d > MAXD) return false;
         } else if (kBinMask & b) {
@@ -229,7 +231,7 @@ template <int K, int W, int MAXD> struct Lean {
                     else if (op == PDOP_RDIVC) O::rdivc(acc[q], rd_imm(prog + pc + 1));
                     else if (op == PDOP_SQRT) O::sqrtj(acc[q]);
                     else if (op == PDOP_LOG) O::logj(acc[q]);
-                    else if (op == PDOP_POWN) O::pown(acc[q], pn);
+                    else if (op == PDOP_POWN) pown_lean(acc[q], pn);
                     else absj<K>(acc[q]);
                 }
             }
@@ -237,6 +239,28 @@ template <int K, int W, int MAXD> struct Lean {
             first = false;
             pc = npc;
             w = wn;
+        }
+    }
+
+    // JetOps::pown for 2 <= n <= 8 (lean_prescan admits no other), the same arithmetic, with
+    // no loop: JetOps::pown's repeated-multiplication loop for n > 4, nested in the interpreter
+    // loop, made the register allocator copy the whole accumulator jet on every back edge
+    // (14 v_mov_b64 per opcode, ~10 % of pass 1); the guarded products below are unrolled
+    static __device__ __forceinline__ void pown_lean(J& t, int n) {
+        if (n <= 4) {
+            if (n == 3) {
+                const J base = t;
+                O::square(t);
+                O::mul(base, t);
+            } else {
+                O::square(t);
+                if (n == 4) O::square(t);
+            }
+        } else {
+            const J base = t;
+#pragma unroll
+            for (int k = 1; k < 8; ++k)
+                if (k < n) O::mul(base, t);
         }
     }
 
