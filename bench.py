@@ -64,14 +64,13 @@ def pmc_traffic(n_per_launch, dominant=DOMINANT):
     (profiles/*_pmc.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc
     passes), scaled to this launch's candidate count; None if there is none."""
     files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        s = json.load(f)
-    k = s.get('kernels', {}).get(dominant)
-    if not k or not k.get('candidates'):
-        return None, os.path.basename(files[-1])
-    return k['hbm_bytes_per_launch'] / k['candidates'] * n_per_launch, os.path.basename(files[-1])
+    for path in reversed(files):          # the newest summary (by name) that has the kernel
+        with open(path) as f:
+            s = json.load(f)
+        k = s.get('kernels', {}).get(dominant)
+        if k and k.get('candidates') and 'hbm_bytes_per_launch' in k:
+            return k['hbm_bytes_per_launch'] / k['candidates'] * n_per_launch, os.path.basename(path)
+    return None, None
 
 
 def main():

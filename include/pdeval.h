@@ -136,9 +136,9 @@ typedef struct pdeval_params {
     double point_abs_tol;/* force-free point stage: a residual that is certainly non-zero
                             rejects if it is rational (an exact Number != 0) or if
                             |det| >= point_abs_tol = 1e-20 (validator.py:371-397)     */
-    double res_rel_acc;  /* point stage: a residual decided in fp64 must carry a bound
-                            noise_kappa x noise <= res_rel_acc x |res| (1e-11), else it
-                            is re-evaluated in double-double          */
+    double res_rel_acc;  /* point stage: a residual decided in fp64 must carry a
+                            first-order error bound noise <= res_rel_acc x |res| (1e-11),
+                            else it is re-evaluated in double-double  */
 } pdeval_params;
 
 /* Per-candidate outputs; any pointer may be NULL (not produced).  Host or device memory

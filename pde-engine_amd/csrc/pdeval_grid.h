@@ -314,8 +314,13 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
     }
 }
 
+// waves per SIMD of pass 1: force-free 4 (116 VGPRs; 5 waves spill 96 B/lane and measured
+// 85.6 vs 84.2 ms), Kerr 5 (49.9 vs 56.7 ms at 4)
 #ifndef PD_GRID_WAVES_PER_SIMD
 #define PD_GRID_WAVES_PER_SIMD 4
+#endif
+#ifndef PD_KERR_WAVES_PER_SIMD
+#define PD_KERR_WAVES_PER_SIMD 5
 #endif
 #ifndef PD_KERR_W
 #define PD_KERR_W 2
@@ -429,8 +434,8 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
 // pass 1: one wave per candidate, 4 per 256-thread block; a.defer_list takes stack-3+ programs,
 // slow_list what the lean path does not take (drained by the generic kernel)
 template <int PROB>
-__global__ __launch_bounds__(256, PD_GRID_WAVES_PER_SIMD) void grid_kernel(KernelArgs a, int64_t* slow_list,
-                                                                          int32_t* slow_count) {
+__global__ __launch_bounds__(256, PROB == PDEVAL_PROBLEM_FORCE_FREE ? PD_GRID_WAVES_PER_SIMD : PD_KERR_WAVES_PER_SIMD)
+void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
 #ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
 #else

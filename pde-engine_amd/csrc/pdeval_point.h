@@ -10,7 +10,8 @@
 // Here every reference point is evaluated with the error-bounded interpreter (pdeval_tier2.h),
 // which carries a first-order bound `noise` of the rounding error beside the value:
 //   tier A (fp64): decide where the bound makes the answer certain and the value accurate to
-//           res_rel_acc (1e-11, so the reported residual is within 1e-10 of the exact one);
+//           res_rel_acc (noise <= 1e-11 |res|, so the reported residual is within 1e-10 of the
+//           exact one);
 //           where |res| <= kappa*noise the point passes PROVISIONALLY (P0_PROV): the exact value
 //           may be 0 (a true solution) or a non-zero hidden in fp64 noise;
 //   tier B (double-double, dd.h, at the end of the call): the undecided candidates (P0_DD) and
@@ -123,7 +124,9 @@ __device__ __forceinline__ uint8_t ff_point_rule(double res_abs, double noise, b
                                                  const pdeval_params& prm) {
     const double kn = prm.noise_kappa * noise;
     if (res_abs > kn) {                                    // certainly non-zero
-        const uint8_t acc = (!FINAL && kn > prm.res_rel_acc * res_abs) ? P0_DD : 0;
+        // accuracy of the reported value: the first-order bound itself (kappa is the safety
+        // factor of the zero DECISION; 1e-11 leaves x10 to the 1e-10 requirement)
+        const uint8_t acc = (!FINAL && noise > prm.res_rel_acc * res_abs) ? P0_DD : 0;
         if (rational) return P0_REJECT | acc;             // an exact Number != 0
         if (res_abs - kn >= prm.point_abs_tol) return P0_REJECT | acc;   // |evalf(50)| >= 1e-20
         if (res_abs + kn < prm.point_abs_tol) return P0_PASS | acc;      // non-zero below 1e-20
@@ -139,7 +142,7 @@ template <bool FINAL>
 __device__ __forceinline__ int kerr_point_rule(double res_abs, double noise, const pdeval_params& prm) {
     const double kn = prm.noise_kappa * noise;
     if (FINAL) return res_abs >= prm.kerr_abs_tol ? 1 : 0;
-    const int acc = (res_abs > kn && kn > prm.res_rel_acc * res_abs) ? 4 : 0;
+    const int acc = (res_abs > kn && noise > prm.res_rel_acc * res_abs) ? 4 : 0;
     if (res_abs - kn >= prm.kerr_abs_tol) return 1 | acc;
     if (res_abs + kn < prm.kerr_abs_tol) return 0 | acc;
     return 2;
