@@ -66,6 +66,7 @@ struct pdeval_ctx {
     uint8_t* d_pstate = nullptr;    // point-stage state, capacity cap
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
     double* d_noise = nullptr;      // fp64 noise bounds at the reference points, cap * 4
+    T2Acc* d_t2acc = nullptr;       // tier-2 accumulators, cap entries, zero between launches
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -287,6 +288,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->d_pstate) (void)hipFree(c->d_pstate);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
+    if (c->d_t2acc) (void)hipFree(c->d_t2acc);
     for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) (void)hipFree(p);
@@ -428,6 +430,10 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (c->d_noise) (void)hipFree(c->d_noise);
     c->d_noise = nullptr;
     HIPCHK(c, hipMalloc(&c->d_noise, cap * 4 * sizeof(double)));
+    if (c->d_t2acc) (void)hipFree(c->d_t2acc);
+    c->d_t2acc = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_t2acc, cap * sizeof(T2Acc)));
+    HIPCHK(c, hipMemset(c->d_t2acc, 0, cap * sizeof(T2Acc)));   // tier 2 leaves it zero
     c->cap = cap;
     return PDEVAL_OK;
 }
@@ -438,6 +444,14 @@ template <class T, int K, int MAXD> constexpr size_t stack_lds(int waves) {
 }
 
 // dynamic LDS of one tier-2 wave: (MAXD-1) slots of a value jet (T) and an error jet (f64)
+// waves per tier-2 list entry (pdeval_tier2.h): real lists are long (thousands of entries per
+// 2^20 batch), the complex list short (~150)
+#ifndef PD_T2_PARTS
+#define PD_T2_PARTS 4
+#endif
+#ifndef PD_T2_PARTS_C
+#define PD_T2_PARTS_C 16
+#endif
 template <class T, int K, int MAXD> constexpr size_t tier2_lds() {
     return (size_t)(MAXD - 1) * ((K + 1) * (K + 2) / 2) * 64 * (sizeof(T) + sizeof(double));
 }
@@ -506,6 +520,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.pdeep_list = c->d_list[L_PDEEP];
     a.pdeep_count = cnt + L_PDEEP;
     a.noise_ref = c->d_noise;
+    a.t2acc = c->d_t2acc;
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
     // complex-valued ones -> L_CPLX
@@ -568,12 +583,13 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // tier 2 (pdeval_tier2.h): re-decide every tier-1 grid failure with error bounds, by stack
     KernelArgs t = follow(L_ESC, L_ESC_DEEP, L_ESC);
     mark(7);
-    hipLaunchKernelGGL((tier2_kernel<PROB, double, 2>), dim3((unsigned)std::min<int64_t>(n, 8192)), dim3(64),
-                       (tier2_lds<double, K, 2>()), s, t);
+    // (PARTS waves per entry: pdeval_tier2.h)
+    hipLaunchKernelGGL((tier2_kernel<PROB, double, 2, false, PD_T2_PARTS>), dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS, 8192)),
+                       dim3(64), (tier2_lds<double, K, 2>()), s, t);
     HIPCHK(c, hipGetLastError());
     mark(8);
-    hipLaunchKernelGGL((tier2_kernel<PROB, double, 3>), dim3((unsigned)std::min<int64_t>(n, 4096)), dim3(64),
-                       (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
+    hipLaunchKernelGGL((tier2_kernel<PROB, double, 3, false, PD_T2_PARTS>), dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS, 4096)),
+                       dim3(64), (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
     HIPCHK(c, hipGetLastError());
     mark(9);
     hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
@@ -581,7 +597,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     HIPCHK(c, hipGetLastError());
     if constexpr (FF) {
         mark(10);
-        hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4>), dim3((unsigned)std::min<int64_t>(n, 1024)), dim3(64),
+        hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4, false, PD_T2_PARTS_C>),
+                           dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS_C, 4096)), dim3(64),
                            (tier2_lds<cplx, K, 4>()), s, follow(L_ESC_C, L_ESC_C_DEEP, L_ESC_C));
         HIPCHK(c, hipGetLastError());
         // complex programs of stack 5..8: operand stack in private memory (161 KiB of LDS would

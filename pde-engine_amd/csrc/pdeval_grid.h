@@ -203,17 +203,21 @@ template <int K, int W, int MAXD> struct Lean {
                     }
                 }
             } else if (b & kBinMask) {
-                J l[W];
-                load(stk + (MAXD == 2 ? 0 : d - 2) * SLOT, lane, l);
+                const double* src = stk + (MAXD == 2 ? 0 : d - 2) * SLOT;
                 --d;
+                // one operand jet at a time: W > 2 would not hold W operand jets beside the
+                // W accumulators in registers
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
-                    if (op == PDOP_DIV) O::div(l[q], acc[q]);
-                    else if (op == PDOP_SUB) O::sub(l[q], acc[q]);
-                    else if (op == PDOP_ADD) O::add(l[q], acc[q]);
-                    else if (op == PDOP_MUL) O::mul(l[q], acc[q]);
-                    else if (op == PDOP_RDIV) O::rdiv(l[q], acc[q]);
-                    else O::rsub(l[q], acc[q]);
+                    J l;
+#pragma unroll
+                    for (int c = 0; c < NCJ; ++c) l.c[c] = src[(q * NCJ + c) * 64 + lane];
+                    if (op == PDOP_DIV) O::div(l, acc[q]);
+                    else if (op == PDOP_SUB) O::sub(l, acc[q]);
+                    else if (op == PDOP_ADD) O::add(l, acc[q]);
+                    else if (op == PDOP_MUL) O::mul(l, acc[q]);
+                    else if (op == PDOP_RDIV) O::rdiv(l, acc[q]);
+                    else O::rsub(l, acc[q]);
                 }
             } else if (b & kVarMask) {
 #pragma unroll
@@ -390,17 +394,22 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             const double inv_y = per_row == 1 ? inv_y0 : rcp(y);
             // Kerr: this point's operator coefficients (a 128 KiB table, L2-resident) are loaded
             // before the program runs, so their latency hides under the interpreter
+            // (W > 2: after it, so that 4W doubles are not live through the interpreter)
             double kv[W][4];
-            if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
+            auto load_kv = [&]() {
+                if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
 #pragma unroll
-                for (int q = 0; q < W; ++q) {
-                    const double* kp = a.kc + 4 * (a.n_ref + min(row + q, a.nx - 1) * a.ny + sl * 64 + lane);
+                    for (int q = 0; q < W; ++q) {
+                        const double* kp = a.kc + 4 * (a.n_ref + min(row + q, a.nx - 1) * a.ny + sl * 64 + lane);
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) kv[q][i] = kp[i];
+                        for (int i = 0; i < 4; ++i) kv[q][i] = kp[i];
+                    }
                 }
-            }
+            };
+            if constexpr (W <= 2) load_kv();
             J u[W];
             L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane);
+            if constexpr (W > 2) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {
                 if (W > 1 && row + q >= a.nx) break;                     // uniform

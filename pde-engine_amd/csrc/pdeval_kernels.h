@@ -55,6 +55,15 @@ struct KernelArgs {
     int64_t* pdeep_list;        // real programs deeper than pass 0's stack: the deep point pass
     int32_t* pdeep_count;
     double* noise_ref;          // n * n_ref fp64 noise bounds at the reference points (point stage)
+    struct T2Acc* t2acc;        // tier 2: one accumulator per list entry (pdeval_tier2.h), zeroed
+};
+
+// Partial grid counts of one tier-2 list entry whose grid is split over several waves.
+struct T2Acc {
+    int32_t nb1, nb2, nfin, nnonfin;
+    unsigned long long qmax_bits;   // max of non-negative doubles = max of their bit patterns
+    uint32_t grad;
+    int32_t done;                   // parts merged so far
 };
 
 // Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).

@@ -438,7 +438,14 @@ template <int PROB, class T> __device__ __forceinline__ double residual_noise(co
 #endif
 // PRIV: the operand stack in private memory instead of LDS (complex programs of stack 5..8,
 // whose value + error slots would need 161 KiB of LDS per wave)
-template <int PROB, class T, int MAXD, bool PRIV = false>
+//
+// PARTS: every list entry's grid is split over PARTS waves (contiguous chunk ranges).  One wave
+// per entry left most of the chip idle on short lists (152 complex entries per 2^20 batch kept
+// 152 of 1024 SIMDs busy for 3 ms).  Each part adds its counts into the entry's accumulator
+// (a.t2acc, zero between launches) and the part that completes the entry writes the outputs
+// and zeroes the accumulator again.  Sums of counts and the max of maxima are the values the
+// single-wave loop computes, so the outputs do not depend on PARTS.
+template <int PROB, class T, int MAXD, bool PRIV = false, int PARTS = 1>
 __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
     constexpr int NC = nc(K);
@@ -457,7 +464,9 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
     if constexpr (!PRIV) stk = STK{vs, es, lane};
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
-    for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+    for (int64_t wp = blockIdx.x; wp < nwork * PARTS; wp += gridDim.x) {
+        const int64_t wi = wp / PARTS;
+        const int part = (int)(wp - wi * PARTS);
         const int64_t entry = a.list[wi];
         const int64_t cand = entry & PD_ESC_CAND_MASK;
         const uint32_t flags = (uint32_t)(entry >> PD_ESC_SHIFT);
@@ -467,7 +476,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
         const uint32_t hdr = rd_word(prog);
         const int depth = (int)((hdr >> 8) & 0xffu);
         if (depth > MAXD) {
-            if (lane == 0 && a.defer_list) list_append(a.defer_list, a.defer_count, a.list_capacity, entry);
+            if (part == 0 && lane == 0 && a.defer_list) list_append(a.defer_list, a.defer_count, a.list_capacity, entry);
             continue;
         }
         // ---- point stage (only if it failed tier 1)
@@ -500,10 +509,13 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
         int nbad_out = -1, nb1 = 0, nb2 = 0, nfin = 0, nnonfin = 0;
         double qmax = 0.0;
         const bool eval_grid = !(flags & ESC_GRID_EVAL) || (flags & ESC_GRID_FAIL);
+        if (!eval_grid && part != 0) continue;     // nothing to split: part 0 decides
         if (eval_grid) {
             const int per_row = a.ny >> 6;
             const int nchunks = a.nx * per_row;
-            for (int ch = 0; ch < nchunks; ++ch) {
+            const int ch0 = (int)((int64_t)nchunks * part / PARTS);
+            const int ch1 = (int)((int64_t)nchunks * (part + 1) / PARTS);
+            for (int ch = ch0; ch < ch1; ++ch) {
                 const int row = ch / per_row, sl = ch - row * per_row;
                 const int p = a.n_ref + row * a.ny + sl * 64 + lane;
                 const double x = rd_sf64(a.gx + row);
@@ -531,11 +543,42 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             nfin = wave_sum(nfin);
             nnonfin = wave_sum(nnonfin);
             qmax = wave_max(qmax);
-            nbad_out = nb1 <= a.prm.max_bad ? nb1 : nb2;
         }
+        bool grad_any = __any(grad_nz);
+        if constexpr (PARTS > 1) {
+            if (eval_grid) {
+                // merge this part into the entry's accumulator; the last part carries on
+                int last = 0;
+                if (lane == 0) {
+                    T2Acc* A = a.t2acc + wi;
+                    atomicAdd(&A->nb1, nb1);
+                    atomicAdd(&A->nb2, nb2);
+                    atomicAdd(&A->nfin, nfin);
+                    atomicAdd(&A->nnonfin, nnonfin);
+                    atomicMax(&A->qmax_bits, (unsigned long long)__double_as_longlong(qmax));  // qmax >= 0
+                    if (grad_any) atomicOr(&A->grad, 1u);
+                    __threadfence();
+                    if (atomicAdd(&A->done, 1) == PARTS - 1) {
+                        __threadfence();
+                        nb1 = atomicAdd(&A->nb1, 0);
+                        nb2 = atomicAdd(&A->nb2, 0);
+                        nfin = atomicAdd(&A->nfin, 0);
+                        nnonfin = atomicAdd(&A->nnonfin, 0);
+                        qmax = __longlong_as_double((long long)atomicMax(&A->qmax_bits, 0ull));
+                        grad_any = atomicOr(&A->grad, 0u) != 0u;
+                        A->nb1 = A->nb2 = A->nfin = A->nnonfin = A->done = 0;   // ready for the next launch
+                        A->grad = 0u;
+                        A->qmax_bits = 0ull;
+                        last = 1;
+                    }
+                }
+                if (!__builtin_amdgcn_readfirstlane(last)) continue;   // lane 0 is the first active lane
+            }
+        }
+        if (eval_grid) nbad_out = nb1 <= a.prm.max_bad ? nb1 : nb2;
         // (P0_CONST: a Kerr constant whose gradient is rounding noise -- pdeval_kernels.h)
         const bool pconst = a.pstate && (a.pstate[cand] & P0_CONST);
-        const bool any_grad = (__any(grad_nz) || (flags & ESC_ANY_GRAD)) && !pconst;
+        const bool any_grad = (grad_any || (flags & ESC_ANY_GRAD)) && !pconst;
         if (lane == 0) {
             const bool has_fin = eval_grid ? nfin > 0 : (flags & ESC_NFIN) != 0;
             const bool structural = (PROB != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);

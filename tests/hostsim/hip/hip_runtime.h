@@ -25,6 +25,11 @@ inline void __builtin_amdgcn_sched_barrier(int) {}
 inline int atomicAdd(int32_t* p, int v) { int o = *p; *p += v; return o; }
 inline uint32_t atomicOr(uint32_t* p, uint32_t v) { uint32_t o = *p; *p |= v; return o; }
 inline uint32_t atomicAnd(uint32_t* p, uint32_t v) { uint32_t o = *p; *p &= v; return o; }
+inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) {
+    unsigned long long o = *p; if (v > o) *p = v; return o; }
+inline void __threadfence() {}
+inline long long __double_as_longlong(double v) { long long r; __builtin_memcpy(&r, &v, 8); return r; }
+inline double __longlong_as_double(long long v) { double r; __builtin_memcpy(&r, &v, 8); return r; }
 inline double __hiloint2double(int hi, int lo) {
     uint64_t b = ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
     double d;

@@ -108,3 +108,74 @@ def test_worker_with_run_database_and_writer(tmp_path):
     assert rep['valid'] == sum(ok[e] for e, *_ in items)
     names = {name for _, name in rep['paper_solutions']}
     assert {'Vertical field', 'X-point', 'Radial', 'Dipolar', 'Parabolic', 'Bent'} <= names, names
+
+
+def _driver_rows():
+    import json
+    import os
+    p = os.path.join(os.path.dirname(__file__), 'golden', 'ref', 'driver_ff_d2_rows.jsonl')
+    with open(p) as f:
+        return [json.loads(l) for l in f]
+
+
+def test_reference_driver_inline_rows():
+    """The reference driver's own run table (``--max-depth 2 --validators 0``, the rows it
+    completed; tests/golden/gen_driver_rows.py) replayed through its inline loop
+    (general_method_paper_reproduction.py:1288-1365) with this plugin as ``discovery.validator``:
+    every row gets the same validation_status, is_valid and validation_reason text."""
+    import sympy as sp
+    from problems import load_problem
+    prob = load_problem('force_free')
+    locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
+    coords = [prob.symbols.get(n, sp.Symbol(n)) for n in ('rho', 'z', 'r', 'x')]
+    rows = _driver_rows()
+    assert len(rows) == 50
+    for r in rows:
+        u = sp.sympify(r['expression'], locals=locs)
+        if not any(u.has(c) for c in coords):                              # :1292-1294
+            ok, reason = False, 'constant-only (skipped)'
+        else:
+            try:                                                            # :1299-1316
+                ok, reason = prob.validator.validate(u, check_regularity=False, fast_point_only=False,
+                                                     lean_first=True, defer_heavy_checks=True,
+                                                     enforce_anchor=False)
+            except TypeError:
+                ok, reason = prob.validator.validate(u, check_regularity=False, fast_point_only=False)
+        status = 'completed' if ok is not None else 'error'                 # :1358
+        assert (status, int(bool(ok)), reason) == \
+            (r['validation_status'], r['is_valid'], r['validation_reason']), r['expression']
+    desc = prob.validator.describe() if hasattr(prob.validator, 'describe') else {}
+    assert (desc or {}).get('method_name') is None and (desc or {}).get('math_definition') is None
+
+
+def test_reference_driver_rows_through_worker_and_writer(tmp_path):
+    """The same run table rebuilt with the reference's schema (same ids, expressions,
+    normalized keys, signatures, depths, all 'pending'), drained by the GPU worker pool's claim
+    loop and the centralized writer: the rows the reference validated get the same status,
+    is_valid and reason (the constant-only row is skipped before validation by the inline
+    loop only, so it is not compared)."""
+    import os
+    import sqlite3
+    import threading
+    from pdeval import persist
+    from pdeval.worker import validator_worker
+    rows = _driver_rows()
+    db = os.path.join(tmp_path, 'run.db')
+    run_id = 'driver-replay'
+    table = persist.init_run_db(db, run_id, max_depth=2)
+    ids = persist.insert_candidates(db, table, [(r['expression'], r['normalized'], r['signature'], r['depth'])
+                                                for r in rows])
+    assert ids == [r['id'] for r in rows]
+    rq = queue.Queue()
+    wt = threading.Thread(target=persist.result_writer, args=(run_id, table, db, rq), kwargs={'poll_s': 0.05})
+    wt.start()
+    n = validator_worker(run_id, table, db, 'force_free', None, rq, batch_size=16, idle_exit_s=1.0)
+    rq.put(None)
+    wt.join(timeout=60)
+    assert n == len(rows)
+    got = {r[0]: r[1:] for r in sqlite3.connect(db).execute(
+        f'SELECT id, validation_status, is_valid, validation_reason FROM {table}')}
+    for r in rows:
+        if r['validation_reason'] == 'constant-only (skipped)':
+            continue
+        assert got[r['id']] == (r['validation_status'], r['is_valid'], r['validation_reason']), r['expression']
