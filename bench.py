@@ -114,7 +114,8 @@ def main():
     total = a.n * world
     rng = np.random.default_rng(0)
     tiled = np.tile(np.arange(nprog, dtype=np.int64), (total + nprog - 1) // nprog)[:total]
-    rng.shuffle(tiled)
+    if not os.environ.get('PD_BENCH_STREAM_ORDER'):   # (experiment: keep the stream order)
+        rng.shuffle(tiled)
 
     # algorithmic work of the batch; it also balances the shards
     lib = _lib.load()

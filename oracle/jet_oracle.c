@@ -406,7 +406,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
             else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;
             else if (nb > prm->max_bad) cls = PDEVAL_CLS_REJECT_GRID;
             else if (problem == PDEVAL_PROBLEM_FORCE_FREE && prm->strict_symbolic &&
-                     (hdr & PDEVAL_FLAG_NONSMOOTH2D)) cls = PDEVAL_CLS_REJECT_SYMBOLIC;
+                     (hdr & (PDEVAL_FLAG_NONSMOOTH2D | PDEVAL_FLAG_UNPROVABLE))) cls = PDEVAL_CLS_REJECT_SYMBOLIC;
             else cls = PDEVAL_CLS_ACCEPT;
         }
         if (status) status[ci] = (uint8_t)cls;

@@ -1156,6 +1156,16 @@ int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t le
         if (!(xs || ys)) hdr |= PDEVAL_FLAG_NOCOORD;
         if (L.det_rational(ir)) hdr |= PDEVAL_FLAG_RATIONAL;
         if (xs && ys && ab) hdr |= PDEVAL_FLAG_NONSMOOTH2D;
+        // SymPy keeps exp(g)**(p/4) unevaluated, and the expand() of the reference's symbolic
+        // stage then leaves terms like exp(g)**(27/2) - exp(9 g)*exp(g)**(9/2) un-merged: it
+        // rejects these u although det == 0 (all 18 of the depth-4 stream: p > 0 rejected,
+        // p < 0 accepted; tests/golden/ref/ff_d4_exp_quarter.jsonl)
+        {
+            const Node& R = C.N(root);
+            if (R.k == POW && C.N(R.a[0]).k == EXP && C.N(R.a[1]).k == NUM && C.N(R.a[1]).r.q == 4 &&
+                C.N(R.a[1]).r.p > 0)
+                hdr |= PDEVAL_FLAG_UNPROVABLE;
+        }
         out.clear();
         out.push_back((int32_t)hdr);
         out.insert(out.end(), E.w.begin(), E.w.end());

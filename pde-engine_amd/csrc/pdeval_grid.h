@@ -297,7 +297,7 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
     else if (nbad > a.prm.max_bad) {
         cls = PDEVAL_CLS_REJECT_GRID;
         esc = ESC_GRID_EVAL | ESC_GRID_FAIL;
-    } else if (prob == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic && (hdr & PDEVAL_FLAG_NONSMOOTH2D)) {
+    } else if (prob == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic && (hdr & (PDEVAL_FLAG_NONSMOOTH2D | PDEVAL_FLAG_UNPROVABLE))) {
         cls = PDEVAL_CLS_REJECT_SYMBOLIC;
     } else {
         cls = PDEVAL_CLS_ACCEPT;

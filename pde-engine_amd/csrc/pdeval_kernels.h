@@ -1005,7 +1005,7 @@ void validate_kernel(KernelArgs a) {
                     cls = PDEVAL_CLS_REJECT_GRID;
                     esc = ESC_GRID_EVAL | ESC_GRID_FAIL;
                 } else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic &&
-                           (hdr & PDEVAL_FLAG_NONSMOOTH2D)) {
+                           (hdr & (PDEVAL_FLAG_NONSMOOTH2D | PDEVAL_FLAG_UNPROVABLE))) {
                     cls = PDEVAL_CLS_REJECT_SYMBOLIC;
                 } else {
                     cls = PDEVAL_CLS_ACCEPT;

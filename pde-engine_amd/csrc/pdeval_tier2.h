@@ -585,7 +585,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             int cls;
             if (!any_grad && has_fin && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
             else if (nbad_out > a.prm.max_bad) cls = PDEVAL_CLS_REJECT_GRID;
-            else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic && (hdr & PDEVAL_FLAG_NONSMOOTH2D))
+            else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic && (hdr & (PDEVAL_FLAG_NONSMOOTH2D | PDEVAL_FLAG_UNPROVABLE)))
                 cls = PDEVAL_CLS_REJECT_SYMBOLIC;
             else cls = PDEVAL_CLS_ACCEPT;
             if (a.out.status) a.out.status[cand] = (uint8_t)cls;

@@ -30,7 +30,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import sympy as sp
 
 from .opcodes import (PDOP, HAS_IMM, IMM_DD, P_OPS, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD,
-                      FLAG_RATIONAL, FLAG_NONSMOOTH2D, op_len)
+                      FLAG_RATIONAL, FLAG_NONSMOOTH2D, FLAG_UNPROVABLE, op_len)
 
 
 class Unsupported(Exception):
@@ -421,14 +421,19 @@ def _det_kind(n):
     if k == 'c':
         return 'R' if n[3] else 'C'
     if k == 'i':
-        return None
-    if k in ('neg', 'abs'):
+        return 'I'               # a factor I scales det by I**6 = -1 (det is homogeneous)
+    if k == 'neg':
         return _det_kind(n[1])
+    if k == 'abs':
+        kd = _det_kind(n[1])
+        return 'R' if kd == 'I' else kd
     if k in ('exp', 'log'):
         return 'C' if _det_kind(n[1]) == 'C' else None
     if k in ('sqrt', 'pown', 'pow'):
         e = Fraction(1, 2) if k == 'sqrt' else (Fraction(n[2]) if k == 'pown' else _frac(n[2]))
         kind = _det_kind(n[1])
+        if kind == 'I':
+            return None if e.denominator != 1 else ('I' if e.numerator % 2 else 'R')
         if kind == 'C':
             return 'C'
         if kind == 'R':
@@ -439,6 +444,10 @@ def _det_kind(n):
         return None
     a, b = n[1], n[2]
     ka, kb = _det_kind(a), _det_kind(b)
+    if k in ('mul', 'div'):
+        # I as a factor: a pure constant whose 6th power is rational
+        ka = ('P', (), True) if ka == 'I' else ka
+        kb = ('P', (), True) if kb == 'I' else kb
     if k in ('add', 'sub'):
         if ka == kb and ka in ('R', 'C'):
             return ka
@@ -486,7 +495,7 @@ def det_rational(ir) -> bool:
             continue
         break
     kind = _det_kind(n)
-    if kind in ('R', 'C'):
+    if kind in ('R', 'C', 'I'):
         return True
     return isinstance(kind, tuple) and all((6 * x).denominator == 1 for x in kind[1])
 
@@ -506,7 +515,7 @@ def compile_ir(ir, uses_i: bool = False, rational_consts: bool = True) -> List[i
     ys = any(o in yops or (o in P_OPS and (w >> 16) & 1) for o, w in zip(ops, words))
     has_coord = xs or ys
     nonsmooth2d = xs and ys and PDOP['ABS'] in ops
-    rational = not uses_i and det_rational(ir)
+    rational = det_rational(ir)      # (I enters only as a factor: _det_kind)
     hdr = (PDOP['HEADER'] | (em.dmax << 8) | (FLAG_COMPLEX if uses_i else 0)
            | (0 if has_coord else FLAG_NOCOORD) | (FLAG_RATIONAL if rational else 0)
            | (FLAG_NONSMOOTH2D if nonsmooth2d else 0))
@@ -517,7 +526,18 @@ def flatten(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
             consts: Optional[Dict[sp.Symbol, sp.Basic]] = None) -> List[int]:
     """SymPy expression -> program words (header first).  Raises Unsupported."""
     ir, uses_i, rational_consts = lower(expr, x_sym, y_sym, consts)
-    return compile_ir(ir, uses_i, rational_consts)
+    words = compile_ir(ir, uses_i, rational_consts)
+    if unprovable(expr):
+        words[0] |= FLAG_UNPROVABLE
+    return words
+
+
+def unprovable(expr: sp.Basic) -> bool:
+    """u = exp(g)**(p/4), p > 0: SymPy keeps the power unevaluated and the reference's symbolic
+    stage (force-free validator.py:404-416) cannot reduce det to 0 (pdeval.h
+    PDEVAL_FLAG_UNPROVABLE; every such candidate of the depth-4 stream)."""
+    return (isinstance(expr, sp.Pow) and isinstance(expr.base, sp.exp) and expr.exp.is_Rational
+            and expr.exp.q == 4 and expr.exp.p > 0)
 
 
 def program_depth(words: Sequence[int]) -> int:

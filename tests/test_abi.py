@@ -32,7 +32,7 @@ def test_opcodes_match_header():
                  'UNSUPPORTED', 'BAD_PROGRAM', 'REJECT_SYMBOLIC'):
         m = re.search(rf'PDEVAL_CLS_{name}\s+(\d+)', HEADER)
         assert int(m.group(1)) == getattr(OPC, f'CLS_{name}')
-    for name in ('COMPLEX', 'NOCOORD', 'RATIONAL', 'NONSMOOTH2D'):
+    for name in ('COMPLEX', 'NOCOORD', 'RATIONAL', 'NONSMOOTH2D', 'UNPROVABLE'):
         m = re.search(rf'PDEVAL_FLAG_{name}\s+\(1u << (\d+)\)', HEADER)
         assert (1 << int(m.group(1))) == getattr(OPC, f'FLAG_{name}')
     assert int(re.search(r'PDEVAL_MAX_STACK\s+(\d+)', HEADER).group(1)) == OPC.MAX_STACK
