@@ -262,9 +262,12 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if ((e = hipSetDevice(device_id)) != hipSuccess) return fail("hipSetDevice", e);
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
-    if ((e = hipMalloc(&c->d_gx, nx * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
+    // d_gx holds the abscissae and then their reciprocals 1.0 / gx (correctly rounded, the
+    // value rcp() forms on the device): the grid pass reads 1/x with a scalar load
+    for (int i = 0; i < nx; ++i) gx.push_back(1.0 / gx[i]);
+    if ((e = hipMalloc(&c->d_gx, 2 * nx * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc(&c->d_gy, ny * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
-    if ((e = hipMemcpy(c->d_gx, gx.data(), nx * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
+    if ((e = hipMemcpy(c->d_gx, gx.data(), 2 * nx * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
         return fail("hipMemcpy", e);
     if ((e = hipMemcpy(c->d_gy, gy.data(), ny * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
         return fail("hipMemcpy", e);

@@ -319,12 +319,18 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 }
 
 // waves per SIMD of pass 1: force-free 4 (116 VGPRs; 5 waves spill 96 B/lane and measured
-// 85.6 vs 84.2 ms), Kerr 5 (49.9 vs 56.7 ms at 4)
+// 85.6 vs 84.2 ms), Kerr 6 (80 VGPRs with the late coefficient loads; 5: 49.0 ms, 6: 46.5)
 #ifndef PD_GRID_WAVES_PER_SIMD
 #define PD_GRID_WAVES_PER_SIMD 4
 #endif
 #ifndef PD_KERR_WAVES_PER_SIMD
-#define PD_KERR_WAVES_PER_SIMD 5
+#define PD_KERR_WAVES_PER_SIMD 6
+#endif
+// Kerr pass 1 loads the operator coefficients after the interpreter: 16 fewer VGPRs live
+// through it, so 6 waves/SIMD fit without spilling (80 VGPRs): pass 1 48.6 -> 46.5 ms
+// (early loads at 6 waves spill 64 B; late loads at 5 waves 49.0, at 7 waves 47.5)
+#ifndef PD_KV_LATE
+#define PD_KV_LATE 1
 #endif
 #ifndef PD_KERR_W
 #define PD_KERR_W 2
@@ -382,12 +388,20 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     double qmax = 0.0;
     int nbad = 0, nfin = 0;
     bool grad_nz = (ps & P0_GRAD) != 0;
+    // grid rows holding a fingerprint point (one bit per row; nx > 64: every row)
+    uint64_t fp_rows = 0;
+#pragma unroll
+    for (int f = 0; f < PDEVAL_FP_N; ++f) {
+        const int r = (a.fp_pts[f] - a.n_ref) / a.ny;
+        if (a.fp_pts[f] >= a.n_ref && r < 64) fp_rows |= 1ull << r;
+    }
+    if (a.nx > 64) fp_rows = ~0ull;
     for (int row = 0; row < a.nx; row += W) {
         double x[W], inv_x[W];
 #pragma unroll
         for (int q = 0; q < W; ++q) {
             x[q] = rd_sf64(a.gx + min(row + q, a.nx - 1));   // a tail row past nx: unused
-            inv_x[q] = rcp(x[q]);
+            inv_x[q] = rd_sf64(a.gx + a.nx + min(row + q, a.nx - 1));   // = rcp(x[q]), host table
         }
         for (int sl = 0; sl < per_row; ++sl) {
             const double y = per_row == 1 ? y0 : a.gy[sl * 64 + lane];
@@ -406,10 +420,11 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                     }
                 }
             };
-            if constexpr (W <= 2) load_kv();
+            constexpr bool kv_late = W > 2 || (MAXD == 2 && PD_KV_LATE);
+            if constexpr (!kv_late) load_kv();
             J u[W];
             L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane);
-            if constexpr (W > 2) load_kv();
+            if constexpr (kv_late) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {
                 if (W > 1 && row + q >= a.nx) break;                     // uniform
@@ -418,7 +433,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u[q].c, x[q]);
                 else r = kerr_epilogue<double>(u[q].c, kv[q]);
                 const double qv = scaled(r.res_abs, r.scale);
-                if (a.out.fingerprint) {
+                if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {
                         const int rel = a.fp_pts[f] - base;   // uniform
