@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -67,6 +68,12 @@ struct pdeval_ctx {
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
     double* d_noise = nullptr;      // fp64 noise bounds at the reference points, cap * 4
     T2Acc* d_t2acc = nullptr;       // tier-2 accumulators, cap entries, zero between launches
+    // shape sort of the batch (pdeval_sort.hip): keys 2 x cap, permutation 2 x cap, scratch
+    bool sort = true;               // env PDEVAL_SORT=0 turns it off (measurements)
+    uint64_t* d_skeys = nullptr;
+    int32_t* d_sidx = nullptr;
+    void* d_stemp = nullptr;
+    size_t stemp_bytes = 0;
     // host-path staging
     int64_t hcap_words = 0, hcap_n = 0;
     int32_t* d_ops = nullptr;
@@ -260,6 +267,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     };
     hipError_t e;
     if ((e = hipSetDevice(device_id)) != hipSuccess) return fail("hipSetDevice", e);
+    if (const char* v = getenv("PDEVAL_SORT")) c->sort = atoi(v) != 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     // d_gx holds the abscissae and then their reciprocals 1.0 / gx (correctly rounded, the
@@ -292,6 +300,9 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
     if (c->d_t2acc) (void)hipFree(c->d_t2acc);
+    if (c->d_skeys) (void)hipFree(c->d_skeys);
+    if (c->d_sidx) (void)hipFree(c->d_sidx);
+    if (c->d_stemp) (void)hipFree(c->d_stemp);
     for (void* p : {(void*)c->d_gx, (void*)c->d_gy, (void*)c->d_kc,
                     (void*)c->d_counts, (void*)c->d_ops, (void*)c->d_off, (void*)c->d_outbuf})
         if (p) (void)hipFree(p);
@@ -437,6 +448,16 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     c->d_t2acc = nullptr;
     HIPCHK(c, hipMalloc(&c->d_t2acc, cap * sizeof(T2Acc)));
     HIPCHK(c, hipMemset(c->d_t2acc, 0, cap * sizeof(T2Acc)));   // tier 2 leaves it zero
+    if (c->d_skeys) (void)hipFree(c->d_skeys);
+    if (c->d_sidx) (void)hipFree(c->d_sidx);
+    if (c->d_stemp) (void)hipFree(c->d_stemp);
+    c->d_skeys = nullptr;
+    c->d_sidx = nullptr;
+    c->d_stemp = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_skeys, 2 * cap * sizeof(uint64_t)));
+    HIPCHK(c, hipMalloc(&c->d_sidx, 2 * cap * sizeof(int32_t)));
+    c->stemp_bytes = sort_temp_bytes(cap);
+    HIPCHK(c, hipMalloc(&c->d_stemp, c->stemp_bytes ? c->stemp_bytes : 16));
     c->cap = cap;
     return PDEVAL_OK;
 }
@@ -526,8 +547,17 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.t2acc = c->d_t2acc;
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
-    // complex-valued ones -> L_CPLX
+    // complex-valued ones -> L_CPLX.  Lanes take the candidates sorted by opcode sequence
+    // (pdeval_sort.hip; the sort is part of pass 0's time)
     mark(0);
+    if (c->sort && n > 1) {
+        const int rc = sort_batch(d_ops, d_off, n_words, n, c->d_skeys, c->d_sidx, c->d_stemp, c->stemp_bytes, s);
+        if (rc != 0) {
+            c->err = std::string("shape sort: ") + hipGetErrorString((hipError_t)rc);
+            return PDEVAL_ERR_HIP;
+        }
+        a.perm = c->d_sidx + n;
+    }
     hipLaunchKernelGGL((point_kernel<PROB>), dim3((unsigned)((n + 255) / 256)), dim3(256),
                        (size_t)4 * 2 * nc(K) * 64 * sizeof(double), s, a);
     HIPCHK(c, hipGetLastError());

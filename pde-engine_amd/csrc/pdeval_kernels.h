@@ -56,6 +56,7 @@ struct KernelArgs {
     int32_t* pdeep_count;
     double* noise_ref;          // n * n_ref fp64 noise bounds at the reference points (point stage)
     struct T2Acc* t2acc;        // tier 2: one accumulator per list entry (pdeval_tier2.h), zeroed
+    const int32_t* perm;        // order of pass 0 and the tier-B collect pass (pdeval_sort.hip), or NULL
 };
 
 // Partial grid counts of one tier-2 list entry whose grid is split over several waves.

@@ -22,4 +22,9 @@ void launch_grid(int problem, unsigned blocks, hipStream_t s, const KernelArgs& 
                  int64_t* slow_list, int32_t* slow_count);
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
                       int64_t* slow_list, int32_t* slow_count);
+// sort the batch by opcode sequence (pdeval_sort.hip): keys/idx hold 2 x n each, the
+// permutation ends in idx + n
+size_t sort_temp_bytes(int64_t cap);
+int sort_batch(const int32_t* ops, const int64_t* offsets, int64_t n_words, int64_t n, uint64_t* keys,
+               int32_t* idx, void* temp, size_t temp_bytes, hipStream_t s);
 }  // namespace pd

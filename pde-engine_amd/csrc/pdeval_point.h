@@ -237,8 +237,9 @@ __global__ __launch_bounds__(256, 1) void point_kernel(KernelArgs a) {
     double* vs = reinterpret_cast<double*>(pd_lds) + (size_t)wib * 2 * (MAXD - 1) * NC * 64;
     double* es = vs + (size_t)(MAXD - 1) * NC * 64;
     LdsStack<double, NC> stk{vs, es, lane};
-    const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cand >= a.n) return;
+    const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= a.n) return;
+    const int64_t cand = a.perm ? (int64_t)a.perm[li] : li;   // lanes take programs sorted by shape
     int64_t beg, end;
     uint8_t ps = P0_NONE;
     if (prog_bounds(a, cand, &beg, &end)) {
@@ -317,8 +318,9 @@ __global__ __launch_bounds__(64, 1) void point_list_kernel(KernelArgs a) {
 // passes whose final class is a grid reject (that class may really be a point reject).
 template <int PROB>
 __global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a, const uint8_t* status) {
-    const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (cand >= a.n) return;
+    const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= a.n) return;
+    const int64_t cand = a.perm ? (int64_t)a.perm[li] : li;   // lists in shape order
     const uint8_t ps = a.pstate[cand];
     if ((ps & 3) == P0_NONE) return;
     const uint8_t st = status[cand];
