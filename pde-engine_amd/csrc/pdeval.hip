@@ -577,7 +577,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 1: programs whose stack fits 2 jets (99 % of force-free depth 4), one wave per
     // candidate; deeper programs go to L_DEFER, tier-1 grid failures to L_ESC
     mark(2);
-    launch_grid(PROB, (unsigned)blocks, s, a, c->d_list[L_SLOW], cnt + L_SLOW);
+    launch_grid(PROB, n, s, a, c->d_list[L_SLOW], cnt + L_SLOW);
     HIPCHK(c, hipGetLastError());
     // what the lean pass did not take (normally nothing): the generic kernel, same pass slot
     hipLaunchKernelGGL((validate_kernel<PROB, double, 2, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),

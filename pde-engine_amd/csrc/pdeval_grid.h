@@ -457,8 +457,20 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
 
 // pass 1: one wave per candidate, 4 per 256-thread block; a.defer_list takes stack-3+ programs,
 // slow_list what the lean path does not take (drained by the generic kernel)
+// Waves (candidates) per pass-1 block: one.  A block's LDS is released only when its last wave
+// ends, and the waves of a 4-wave block ran programs of unrelated lengths, so finished waves
+// left their share idle until the slowest one ended.  With one wave per block:
+// force-free pass 1 83.6 -> 76.6 ms, Kerr 46.8 -> 38.0 ms (profiles/r02_bench_*_wpb*.log).
+// PD_GRID_PERM = 1 instead keeps 4-wave blocks but takes the candidates in the shape order of
+// pdeval_sort.hip, so a block's waves run programs of one opcode sequence (78.3 / 43.9 ms).
+#ifndef PD_GRID_WPB
+#define PD_GRID_WPB 1
+#endif
+#ifndef PD_GRID_PERM
+#define PD_GRID_PERM 0
+#endif
 template <int PROB>
-__global__ __launch_bounds__(256, PROB == PDEVAL_PROBLEM_FORCE_FREE ? PD_GRID_WAVES_PER_SIMD : PD_KERR_WAVES_PER_SIMD)
+__global__ __launch_bounds__(64 * PD_GRID_WPB, PROB == PDEVAL_PROBLEM_FORCE_FREE ? PD_GRID_WAVES_PER_SIMD : PD_KERR_WAVES_PER_SIMD)
 void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
 #ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
@@ -467,8 +479,9 @@ void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
 #endif
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double* stk = reinterpret_cast<double*>(pd_lds) + (size_t)wib * grid_lds<PROB, 2>(1) / sizeof(double);
-    const int64_t cand = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
-    if (cand >= a.n) return;
+    const int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
+    if (wi >= a.n) return;
+    const int64_t cand = (PD_GRID_PERM && a.perm) ? (int64_t)__builtin_amdgcn_readfirstlane(a.perm[wi]) : wi;
     grid_body<PROB, 2>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
 }
 

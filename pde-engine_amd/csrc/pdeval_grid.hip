@@ -7,14 +7,15 @@
 
 namespace pd {
 
-void launch_grid(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
+void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                  int64_t* slow_list, int32_t* slow_count) {
+    const unsigned blocks = (unsigned)((n + PD_GRID_WPB - 1) / PD_GRID_WPB);
     if (problem == PDEVAL_PROBLEM_FORCE_FREE)
-        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(256),
-                           (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2>(4)), s, a, slow_list, slow_count);
+        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(64 * PD_GRID_WPB),
+                           (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2>(PD_GRID_WPB)), s, a, slow_list, slow_count);
     else
-        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(256),
-                           (grid_lds<PDEVAL_PROBLEM_KERR, 2>(4)), s, a, slow_list, slow_count);
+        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(64 * PD_GRID_WPB),
+                           (grid_lds<PDEVAL_PROBLEM_KERR, 2>(PD_GRID_WPB)), s, a, slow_list, slow_count);
 }
 
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,

@@ -16,9 +16,9 @@ void launch_dd_point(int problem, int kind, unsigned grid, hipStream_t s, const 
 // diagnostic: one program at the reference points in precision tier 0..3 (pdeval_point_eval)
 void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a, const int32_t* prog,
                        int plen, double* out, uint8_t* state);
-// the lean grid passes (pdeval_grid.hip): pass 1 over all candidates (256-thread blocks, 4
-// candidates each, stack <= 2), pass 2 persistent over the stack-3 list a.list (64-thread blocks)
-void launch_grid(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
+// the lean grid passes (pdeval_grid.hip): pass 1 over all n candidates (one wave each, stack
+// <= 2), pass 2 persistent over the stack-3 list a.list (64-thread blocks)
+void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                  int64_t* slow_list, int32_t* slow_count);
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
                       int64_t* slow_list, int32_t* slow_count);
