@@ -332,6 +332,12 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 #ifndef PD_KV_LATE
 #define PD_KV_LATE 1
 #endif
+#ifndef PD_KV_LATE_DEEP
+#define PD_KV_LATE_DEEP 0
+#endif
+#ifndef PD_LIST_WAVES_PER_SIMD
+#define PD_LIST_WAVES_PER_SIMD 1
+#endif
 #ifndef PD_KERR_W
 #define PD_KERR_W 2
 #endif
@@ -420,7 +426,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                     }
                 }
             };
-            constexpr bool kv_late = W > 2 || (MAXD == 2 && PD_KV_LATE);
+            constexpr bool kv_late = W > 2 || (MAXD == 2 && PD_KV_LATE) || (MAXD > 2 && PD_KV_LATE_DEEP);
             if constexpr (!kv_late) load_kv();
             J u[W];
             L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane);
@@ -487,7 +493,7 @@ void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
 
 // pass 2: the stack-3 list a.list (count *a.list_count), persistent 64-thread blocks
 template <int PROB>
-__global__ __launch_bounds__(64) void grid_list_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
+__global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST_WAVES_PER_SIMD) void grid_list_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
 #ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
 #else

@@ -7,7 +7,7 @@ T=${TAG:-x}
 for v in "" ${VARS}; do
   L=pde-engine_amd/lib/libpdeval$v.so
   [ -f $L ] || continue
-  PDEVAL_LIB=$L timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu --no-extras > gpurun_out/v/${T}_ff$v.log 2>&1 || exit 5
+  [ -n "$NOFF" ] || PDEVAL_LIB=$L timeout -k 10 200 python bench.py --steps 3 --warmup 1 --no-cpu --no-extras > gpurun_out/v/${T}_ff$v.log 2>&1 || exit 5
   PDEVAL_LIB=$L timeout -k 10 200 python bench.py --problem kerr_magnetosphere --steps 3 --warmup 1 --no-cpu --no-extras > gpurun_out/v/${T}_kerr$v.log 2>&1 || exit 6
 done
 echo VAR_DONE
