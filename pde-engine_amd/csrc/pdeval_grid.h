@@ -472,6 +472,9 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
 #ifndef PD_GRID_WPB
 #define PD_GRID_WPB 1
 #endif
+#ifndef PD_GRID_XCD
+#define PD_GRID_XCD 1
+#endif
 #ifndef PD_GRID_PERM
 #define PD_GRID_PERM 0
 #endif
@@ -485,7 +488,18 @@ void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
 #endif
     const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     double* stk = reinterpret_cast<double*>(pd_lds) + (size_t)wib * grid_lds<PROB, 2>(1) / sizeof(double);
-    const int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + wib;
+    // Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.  One-wave
+    // blocks in launch order would send neighbouring candidates -- whose programs share cache
+    // lines -- to 8 different L2s; instead each XCD takes a contiguous range of blocks.
+    // Force-free: HBM traffic 518 -> 187 B per candidate at the same time (76.0 ms); Kerr
+    // measured 38.0 -> 38.7 ms with it, so Kerr keeps the launch order
+    // (profiles/r02_bench_*_xcd*.log, r02_xcd_ff_pmc.json).
+    int64_t blk = blockIdx.x;
+    if (PD_GRID_XCD && PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+        const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + (x < r ? x : r) + blk / 8;
+    }
+    const int64_t wi = blk * (blockDim.x >> 6) + wib;
     if (wi >= a.n) return;
     const int64_t cand = (PD_GRID_PERM && a.perm) ? (int64_t)__builtin_amdgcn_readfirstlane(a.perm[wi]) : wi;
     grid_body<PROB, 2>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
