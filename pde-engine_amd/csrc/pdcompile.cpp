@@ -970,10 +970,58 @@ struct Lower {
 
     // ---- det_rational (flatten.py _det_kind / det_rational)
     struct Kd {
-        int t;                    // 0 = None, 1 = 'R', 2 = 'C', 3 = ('P', exps, pure)
+        int t;                    // 0 = None, 1 = 'R', 2 = 'C', 3 = ('P', exps, pure, sig)
         std::vector<Rat> ex;
         bool pure = false;
+        // sig: prod h**a, exponents summed per base (flatten.py _sig); bases are IR subtrees
+        // compared structurally (the IR is not hash-consed)
+        std::vector<std::pair<int, Rat>> sig;
     };
+    bool same(int i, int j) const {
+        if (i == j) return true;
+        if (i < 0 || j < 0) return false;
+        const IR &x = ir[i], &y = ir[j];
+        if (x.k != y.k || x.n != y.n || x.irr != y.irr || x.r.p != y.r.p || x.r.q != y.r.q ||
+            x.alpha.p != y.alpha.p || x.alpha.q != y.alpha.q || !(x.c == y.c) || !(x.lo == y.lo))
+            return false;
+        return same(x.a, y.a) && same(x.b, y.b);
+    }
+    std::vector<std::pair<int, Rat>> mksig(const std::vector<std::pair<int, Rat>>& pairs) const {
+        std::vector<std::pair<int, Rat>> acc;
+        for (const auto& pr : pairs) {
+            bool found = false;
+            for (auto& q : acc)
+                if (same(q.first, pr.first)) { q.second = radd(q.second, pr.second); found = true; break; }
+            if (!found) acc.push_back(pr);
+        }
+        std::vector<std::pair<int, Rat>> out;
+        for (const auto& q : acc) if (q.second.p != 0) out.push_back(q);
+        return out;
+    }
+    // the irrational part: exponents modulo 1, integer powers dropped (flatten.py _irr)
+    std::vector<std::pair<int, Rat>> irr(const std::vector<std::pair<int, Rat>>& sg) const {
+        std::vector<std::pair<int, Rat>> out;
+        for (const auto& q : sg) {
+            Rat f = q.second;
+            int64_t m = f.p % f.q;
+            if (m < 0) m += f.q;
+            if (m != 0) out.push_back({q.first, Rat{m, f.q}});
+        }
+        return out;
+    }
+    bool same_irr(const Kd& a, const Kd& b) const {
+        const auto ia = irr(a.sig), ib = irr(b.sig);
+        if (ia.empty() || ia.size() != ib.size()) return false;
+        std::vector<bool> used(ib.size(), false);
+        for (const auto& p : ia) {
+            bool ok = false;
+            for (size_t k = 0; k < ib.size(); ++k)
+                if (!used[k] && same(p.first, ib[k].first) && p.second.p == ib[k].second.p &&
+                    p.second.q == ib[k].second.q) { used[k] = true; ok = true; break; }
+            if (!ok) return false;
+        }
+        return true;
+    }
     Kd kind(int i) {
         const IR& x = ir[i];
         switch (x.k) {
@@ -987,13 +1035,15 @@ struct Lower {
                 if (k.t == 2) return Kd{2, {}, false};
                 if (k.t == 1) {
                     if (rint(e)) return Kd{1, {}, false};
-                    return Kd{3, {e}, true};
+                    return Kd{3, {e}, true, mksig({{x.a, e}})};
                 }
                 if (k.t == 3 && k.pure) {
                     std::vector<Rat> ex;
                     for (Rat a : k.ex) { Rat m = rmul(a, e); if (!rint(m)) ex.push_back(m); }
                     if (ex.empty()) return Kd{1, {}, false};
-                    return Kd{3, ex, true};
+                    std::vector<std::pair<int, Rat>> sg;
+                    for (const auto& q : k.sig) sg.push_back({q.first, rmul(q.second, e)});
+                    return Kd{3, ex, true, mksig(sg)};
                 }
                 return Kd{0, {}, false};
             }
@@ -1003,6 +1053,11 @@ struct Lower {
         Kd ka = kind(a), kb = kind(b);
         if (x.k == IADD || x.k == ISUB) {
             if (ka.t == kb.t && (ka.t == 1 || ka.t == 2)) return Kd{ka.t, {}, false};
+            if (ka.t == 3 && kb.t == 3 && same_irr(ka, kb)) {   // r1*H + r2*H = (r1 + r2)*H
+                std::vector<Rat> ex = ka.ex;
+                ex.insert(ex.end(), kb.ex.begin(), kb.ex.end());
+                return Kd{3, ex, false, ka.sig};
+            }
             if (((ka.t == 1 && kb.t == 2) || (ka.t == 2 && kb.t == 1)) &&
                 ((ka.t == 1 && ir[a].k == IC) || (kb.t == 1 && ir[b].k == IC)))
                 return Kd{2, {}, false};
@@ -1011,11 +1066,14 @@ struct Lower {
         if (ka.t == 0 || kb.t == 0 || ka.t == 2 || kb.t == 2) return Kd{0, {}, false};
         if (ka.t == 1 && kb.t == 1) return Kd{1, {}, false};
         std::vector<Rat> ex = ka.t == 3 ? ka.ex : std::vector<Rat>{};
-        if (kb.t == 3)
+        std::vector<std::pair<int, Rat>> sg = ka.t == 3 ? ka.sig : std::vector<std::pair<int, Rat>>{};
+        if (kb.t == 3) {
             for (Rat r : kb.ex) ex.push_back(x.k == IDIV ? rneg(r) : r);
+            for (const auto& q : kb.sig) sg.push_back({q.first, x.k == IDIV ? rneg(q.second) : q.second});
+        }
         const bool pa = (ka.t == 1 && ir[a].k == IC) || (ka.t == 3 && ka.pure);
         const bool pb = (kb.t == 1 && ir[b].k == IC) || (kb.t == 3 && kb.pure);
-        return Kd{3, ex, pa && pb};
+        return Kd{3, ex, pa && pb, mksig(sg)};
     }
     bool det_rational(int root) {
         int n = root;

@@ -86,6 +86,43 @@ def reason_for(problem_id: int, cls: int, res_ref: Sequence[float], q_ref: float
     return False, 'Error: malformed program'
 
 
+def symbolic_zero_gradient(pd, items, out) -> List[int]:
+    """Force-free: the reference's zero-gradient test is symbolic -- ``u.diff(rho) == 0 and
+    u.diff(z) == 0`` on SymPy's tree (``problems/force_free/validator.py:305-312``).  SymPy can
+    keep a constant u unevaluated while its derivative cancels term by term: in
+    ``exp_neg(rho**2 + z**2)*exp(rho**2)*exp(z**2)`` the product stays a product, but the
+    product rule gives ``2*rho*P - 2*rho*P`` = 0, so the reference reports "Zero gradient".
+    The device sees only values, and its structural test (header NOCOORD) misses such u; a
+    constant u whose derivative SymPy does NOT cancel goes on to the determinant, which is 0.
+    So the candidates whose value agrees at the 4 fingerprint points (a constant has no other
+    way to be) and whose class says the grid was evaluated are re-checked here with the
+    reference's own test, and reclassified ZERO_GRADIENT (verdict False) where it holds.
+    ``items`` are SymPy trees or candidate strings; ``out`` the result dict of one validate call
+    (``status``, ``verdict``, ``fingerprint``), updated in place.  Returns the changed rows."""
+    if pd.problem_id != PROBLEM_FORCE_FREE:
+        return []
+    st, fp = out['status'], out['fingerprint']
+    rows = []
+    for i in range(len(st)):
+        if int(st[i]) not in (CLS_ACCEPT, CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC):
+            continue
+        f = fp[i]
+        if not np.all(np.isfinite(f)):
+            continue
+        if float(np.max(f) - np.min(f)) > 1e-9 * max(float(np.max(np.abs(f))), 1e-300):
+            continue
+        try:
+            u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
+            if u.diff(pd.x) == 0 and u.diff(pd.y) == 0:
+                st[i] = CLS_ZERO_GRADIENT
+                if 'verdict' in out:
+                    out['verdict'][i] = False
+                rows.append(i)
+        except Exception:   # noqa: BLE001  (a tree SymPy cannot differentiate keeps its class)
+            pass
+    return rows
+
+
 class BatchValidator:
     """One problem on one GPU.  Thread-safe (calls are serialized per context)."""
 
@@ -112,10 +149,11 @@ class BatchValidator:
         if not exprs:
             return []
         ops, off, notes = self.compile(exprs)
-        return self._verdicts(ops, off, notes)
+        return self._verdicts(ops, off, notes, exprs)
 
-    def _verdicts(self, ops, off, notes) -> List[Verdict]:
+    def _verdicts(self, ops, off, notes, items) -> List[Verdict]:
         r = self.run(ops, off)
+        symbolic_zero_gradient(self.pd, items, r)
         out = []
         for i in range(len(off) - 1):
             hdr = int(ops[off[i]])
@@ -137,7 +175,7 @@ class BatchValidator:
             return []
         from .native import compile_strings
         ops, off, notes = compile_strings(self.pd, list(strings), stats=stats)
-        return self._verdicts(ops, off, notes)
+        return self._verdicts(ops, off, notes, list(strings))
 
     def close(self):
         self.ctx.close()

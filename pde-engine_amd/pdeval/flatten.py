@@ -401,6 +401,19 @@ def _frac(v: float) -> Fraction:
     return Fraction(v).limit_denominator(1 << 12)
 
 
+def _sig(pairs) -> tuple:
+    """prod h**a with the exponents summed per base (an IR subtree)."""
+    acc: Dict[tuple, Fraction] = {}
+    for h, a in pairs:
+        acc[h] = acc.get(h, Fraction(0)) + a
+    return tuple(sorted(((h, a) for h, a in acc.items() if a != 0), key=repr))
+
+
+def _irr(sig) -> tuple:
+    """The irrational part of a signature: exponents modulo 1, integer powers dropped."""
+    return tuple((h, a % 1) for h, a in sig if a % 1 != 0)
+
+
 def _det_kind(n):
     """Algebraic shape of a node's value, for "is the force-free determinant rational at a
     rational point" (the reference then says "Invalid (point check != 0)", else prints its
@@ -408,8 +421,10 @@ def _det_kind(n):
 
     'R'  a rational function with rational constants;
     'C'  a constant that may be irrational (E, exp(2), sqrt(2) ...);
-    ('P', (a_1, ...), pure)  r * h_1**a_1 * ... with r, h_k rational functions and rational
-         non-integer a_k (pure: r == 1);
+    ('P', (a_1, ...), pure, sig)  r * h_1**a_1 * ... with r, h_k rational functions and rational
+         non-integer a_k (pure: r == 1); sig, the irrational part: the bases h_k with their
+         exponents summed per base modulo 1 (a sum of two terms with equal sig is r' * the same
+         irrational part, e.g. (1 - rho)*sqrt(rho**2 + z**2));
     None anything else (exp/log of a coordinate expression, I ...).
     Every derivative of r * prod h_k**a_k is prod h_k**a_k times a rational function, and the
     determinant is homogeneous of degree 6 in u's derivatives (validator.py:323-347), so it
@@ -437,20 +452,23 @@ def _det_kind(n):
         if kind == 'C':
             return 'C'
         if kind == 'R':
-            return 'R' if e.denominator == 1 else ('P', (e,), True)
+            return 'R' if e.denominator == 1 else ('P', (e,), True, _sig(((n[1], e),)))
         if isinstance(kind, tuple) and kind[2]:
             ex = tuple(a * e for a in kind[1] if (a * e).denominator != 1)
-            return ('P', ex, True) if ex else 'R'
+            sig = tuple((b, a * e) for b, a in kind[3])
+            return ('P', ex, True, _sig(sig)) if ex else 'R'
         return None
     a, b = n[1], n[2]
     ka, kb = _det_kind(a), _det_kind(b)
     if k in ('mul', 'div'):
         # I as a factor: a pure constant whose 6th power is rational
-        ka = ('P', (), True) if ka == 'I' else ka
-        kb = ('P', (), True) if kb == 'I' else kb
+        ka = ('P', (), True, ()) if ka == 'I' else ka
+        kb = ('P', (), True, ()) if kb == 'I' else kb
     if k in ('add', 'sub'):
         if ka == kb and ka in ('R', 'C'):
             return ka
+        if isinstance(ka, tuple) and isinstance(kb, tuple) and _irr(ka[3]) == _irr(kb[3]) and _irr(ka[3]):
+            return ('P', ka[1] + kb[1], False, ka[3])      # r1*H + r2*H = (r1 + r2)*H
         if {ka, kb} == {'R', 'C'} and ((ka == 'R' and a[0] == 'c') or (kb == 'R' and b[0] == 'c')):
             return 'C'
         return None
@@ -461,11 +479,14 @@ def _det_kind(n):
             return 'R'
         ea = ka[1] if isinstance(ka, tuple) else ()
         eb = kb[1] if isinstance(kb, tuple) else ()
+        sa = ka[3] if isinstance(ka, tuple) else ()
+        sb = kb[3] if isinstance(kb, tuple) else ()
         if k == 'div':
             eb = tuple(-x for x in eb)
+            sb = tuple((h, -x) for h, x in sb)
         pure = (ka == 'R' and a[0] == 'c' or isinstance(ka, tuple) and ka[2]) and \
                (kb == 'R' and b[0] == 'c' or isinstance(kb, tuple) and kb[2])
-        return ('P', ea + eb, bool(pure))
+        return ('P', ea + eb, bool(pure), _sig(sa + sb))
     return None
 
 

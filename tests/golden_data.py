@@ -36,6 +36,12 @@ KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl', 'kerr_d4_s2
 # constant solution excluded", there "PDE residual != 0".  (1 of the 1,024,799
 # candidates of the Kerr depth<=4 stream.)
 KERR_PARAM_CLASS = {'exp(a**2)*exp(2*r)*exp(-2*M*r)'}
+# Force-free candidates whose reject TEXT differs, with the same verdict and the same stage:
+# when the reference's symbolic stage is reached with a determinant whose string is >= 3000
+# characters it expands instead of calling Lean and prints "Invalid (expanded det != 0)"
+# (validator.py:407-426); choosing between the two texts needs SymPy's symbolic det, which this
+# path never builds, so the device prints the Lean text.
+FF_DET_TEXT = {'rho/z - pow_3_2(rho**2/z**2)'}
 
 
 def exact_rows(name='ff_d4_exact_det.jsonl'):

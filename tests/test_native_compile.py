@@ -132,6 +132,8 @@ def test_native_verdicts_match_reference_and_sympy_path(prob, files):
     assert np.array_equal(res['status'], ref['status']), \
         [(strings[i], int(res['status'][i]), int(ref['status'][i]))
          for i in np.flatnonzero(res['status'] != ref['status'])[:10]]
+    from pdeval.batch import symbolic_zero_gradient
+    symbolic_zero_gradient(pd_, strings, res)      # the host step of pdeval.batch
     bad = []
     for i, r in enumerate(rows):
         ok, _ = reason_for(pd_.problem_id, int(res['status'][i]), res['res_ref'][i], res['q_ref'][i],
