@@ -101,16 +101,14 @@ def symbolic_zero_gradient(pd, items, out) -> List[int]:
     (``status``, ``verdict``, ``fingerprint``), updated in place.  Returns the changed rows."""
     if pd.problem_id != PROBLEM_FORCE_FREE:
         return []
-    st, fp = out['status'], out['fingerprint']
+    st = np.asarray(out['status'])
+    fp = np.asarray(out['fingerprint'], dtype=np.float64).reshape(len(st), -1)
+    with np.errstate(invalid='ignore'):
+        flat = (np.all(np.isfinite(fp), axis=1) &
+                (fp.max(axis=1) - fp.min(axis=1) <= 1e-9 * np.maximum(np.abs(fp).max(axis=1), 1e-300)) &
+                np.isin(st, (CLS_ACCEPT, CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC)))
     rows = []
-    for i in range(len(st)):
-        if int(st[i]) not in (CLS_ACCEPT, CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC):
-            continue
-        f = fp[i]
-        if not np.all(np.isfinite(f)):
-            continue
-        if float(np.max(f) - np.min(f)) > 1e-9 * max(float(np.max(np.abs(f))), 1e-300):
-            continue
+    for i in np.flatnonzero(flat):
         try:
             u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
             if u.diff(pd.x) == 0 and u.diff(pd.y) == 0:
