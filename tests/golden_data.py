@@ -26,7 +26,7 @@ def stream(name, with_index=False):
 
 
 FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl', 'ff_d4_s2000.jsonl',
-          'ff_d4_exp_quarter.jsonl')
+          'ff_d4_exp_quarter.jsonl', 'ff_d4_t600.jsonl')
 KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl', 'kerr_d4_s2000.jsonl',
             'kerr_d4_accepts.jsonl')
 # Kerr candidates whose reason class differs from the reference's, with the same verdict: the
