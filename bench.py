@@ -40,23 +40,12 @@ def load_workload(problem):
     # force-free: the depth-4 validated set; Kerr: the whole depth<=4 stream
     # (1,024,799 candidates; the pre-validate filters keep 1,999 of a 2,000 seeded sample, so
     # the stream is what reaches validate to 0.05 %: tests/golden/streams/)
+    from pdeval.workload import load_programs
     for name in (f'{problem}_d4_validated.npz', f'{problem}_d4_stream.npz',
                  f'{problem}_d3_validated.npz'):
-        p = os.path.join(ROOT, 'data', name)
-        if os.path.exists(p):
-            z = np.load(p, allow_pickle=False)
-            return name, z['ops'], z['offsets'], z['exprs']
+        if os.path.exists(os.path.join(ROOT, 'data', name)):
+            return (name,) + tuple(load_programs(name))
     raise FileNotFoundError(f'data/{problem}_d*_*.npz missing')
-
-
-def gather_programs(ops, offsets, idx):
-    """Batch of programs idx[...] (contiguous, in order) from a program table."""
-    lens = (offsets[idx + 1] - offsets[idx]).astype(np.int64)
-    new_off = np.zeros(len(idx) + 1, dtype=np.int64)
-    np.cumsum(lens, out=new_off[1:])
-    starts = np.repeat(offsets[idx], lens)
-    within = np.arange(new_off[-1], dtype=np.int64) - np.repeat(new_off[:-1], lens)
-    return ops[starts + within], new_off
 
 
 def pmc_traffic(n_per_launch, dominant=DOMINANT):
@@ -78,7 +67,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--n', type=int, default=1 << 20, help='candidates per GPU per step')
+    ap.add_argument('--n', type=int, default=1 << 21,
+                    help='candidates per GPU per step (8 GPUs: 2^24, the C4 batch of SURVEY.md §8d)')
     ap.add_argument('--problem', default='force_free')
     ap.add_argument('--early-exit', action='store_true',
                     help='headline run stops after the point stage for point-rejects')
@@ -96,7 +86,8 @@ def main():
     import torch.distributed as dist
     from pdeval import _lib
     from pdeval.opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR, FP_N, FLAG_COMPLEX
-    from pdeval.shard import gather_verdicts, gather_verdicts_native, init_native_comm, shard_ranges
+    from pdeval.shard import gather_verdicts, gather_verdicts_native, init_native_comm
+    from pdeval import workload as WL
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -112,21 +103,13 @@ def main():
     wname, ops_all, off_all, exprs_all = load_workload(slug)
     nprog = len(off_all) - 1
     total = a.n * world
-    rng = np.random.default_rng(0)
-    tiled = np.tile(np.arange(nprog, dtype=np.int64), (total + nprog - 1) // nprog)[:total]
-    if not os.environ.get('PD_BENCH_STREAM_ORDER'):   # (experiment: keep the stream order)
-        rng.shuffle(tiled)
-
+    # (experiment PD_BENCH_STREAM_ORDER: keep the stream order)
+    tiled = WL.tiled_indices(nprog, total, seed=0, shuffle=not os.environ.get('PD_BENCH_STREAM_ORDER'))
     # algorithmic work of the batch; it also balances the shards
-    lib = _lib.load()
-    flops_prog = np.array([lib.pdeval_program_flops(pid, ops_all[off_all[i]:].ctypes.data,
-                                                    int(off_all[i + 1] - off_all[i]))
-                           for i in range(nprog)])
-    ranges = shard_ranges(total, world, weights=flops_prog[tiled] if world > 1 else None)
-    s0, s1 = ranges[rank]
-    idx = tiled[s0:s1]
-    n = len(idx)
-    ops, off = gather_programs(ops_all, off_all, idx)
+    flops_prog = WL.flops_per_program(pid, ops_all, off_all)
+    plan = WL.rank_plan(tiled, world, rank, flops_prog)
+    ranges, idx, n = plan.ranges, plan.idx, plan.n
+    ops, off = WL.gather_programs(ops_all, off_all, idx)
     ctx = _lib.Context(pid, device=local)
     npts, nref = ctx.n_points, ctx.n_ref
     flops_step = float(flops_prog[idx].sum()) * npts
@@ -373,6 +356,7 @@ def cpu_baseline(pid, ops_all, off_all, idx, budget_s):
     workload, one core."""
     import oracle_lib as O
     sample = idx[:4096]
+    from pdeval.workload import gather_programs
     ops, off = gather_programs(ops_all, off_all, sample)
     done, t0 = 0, time.perf_counter()
     while done < len(sample) and time.perf_counter() - t0 < budget_s:

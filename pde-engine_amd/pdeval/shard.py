@@ -59,6 +59,19 @@ def unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:
     return np.unpackbits(np.asarray(bits, dtype=np.uint8), bitorder='little')[:n].astype(bool)
 
 
+def padded_nbytes(ranges: Sequence[Tuple[int, int]]) -> int:
+    """Bytes each rank contributes to the all-gather: the largest shard's packed bitmap."""
+    return max(max(((e - s) + 7) // 8 for s, e in ranges), 1) if ranges else 1
+
+
+def assemble_bits(gathered: np.ndarray, ranges: Sequence[Tuple[int, int]]) -> np.ndarray:
+    """Global bool verdicts from the all-gathered bitmaps (uint8 [world * nbytes], rank r's
+    packed bits at r * nbytes, LSB first as the kernel writes them)."""
+    nb = padded_nbytes(ranges)
+    host = np.asarray(gathered, dtype=np.uint8).reshape(len(ranges), nb)
+    return np.concatenate([unpack_bits(host[r], e - s) for r, (s, e) in enumerate(ranges)])
+
+
 def gather_verdicts(local_bits, ranges: Sequence[Tuple[int, int]], group=None):
     """All-gather the per-rank verdict bitmaps and return the global bool[n] on every rank.
 
@@ -70,8 +83,7 @@ def gather_verdicts(local_bits, ranges: Sequence[Tuple[int, int]], group=None):
     import torch
     import torch.distributed as dist
     world = len(ranges)
-    nbytes = max(((e - s) + 7) // 8 for s, e in ranges) if ranges else 0
-    nbytes = max(nbytes, 1)
+    nbytes = padded_nbytes(ranges)
     buf = torch.zeros(nbytes, dtype=torch.uint8, device=local_bits.device)
     k = min(nbytes, local_bits.numel())
     buf[:k] = local_bits.reshape(-1)[:k]
@@ -82,8 +94,7 @@ def gather_verdicts(local_bits, ranges: Sequence[Tuple[int, int]], group=None):
         parts = [torch.empty_like(buf) for _ in range(world)]
         dist.all_gather(parts, buf, group=group)
         out = torch.cat(parts)
-    host = out.cpu().numpy().reshape(world, nbytes)
-    return np.concatenate([unpack_bits(host[r], e - s) for r, (s, e) in enumerate(ranges)])
+    return assemble_bits(out.cpu().numpy(), ranges)
 
 
 def init_native_comm(ctx, rank: int, world: int, group=None):
@@ -103,7 +114,7 @@ def gather_verdicts_native(ctx, local_bits, ranges: Sequence[Tuple[int, int]], s
     ``local_bits`` is this rank's packed bitmap as a uint8 torch tensor on the context's GPU."""
     import torch
     world = len(ranges)
-    nbytes = max(max(((e - s) + 7) // 8 for s, e in ranges), 1)
+    nbytes = padded_nbytes(ranges)
     buf = torch.zeros(nbytes, dtype=torch.uint8, device=local_bits.device)
     k = min(nbytes, local_bits.numel())
     buf[:k] = local_bits.reshape(-1)[:k]
@@ -111,5 +122,4 @@ def gather_verdicts_native(ctx, local_bits, ranges: Sequence[Tuple[int, int]], s
     torch.cuda.synchronize(local_bits.device)
     ctx.gather_bits(buf.data_ptr(), nbytes, out.data_ptr(), stream)
     torch.cuda.synchronize(local_bits.device)
-    host = out.cpu().numpy().reshape(world, nbytes)
-    return np.concatenate([unpack_bits(host[r], e - s) for r, (s, e) in enumerate(ranges)])
+    return assemble_bits(out.cpu().numpy(), ranges)

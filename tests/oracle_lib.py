@@ -81,3 +81,30 @@ def point(problem_id, words, x, y, cplx=False):
     if rc:
         raise ValueError(f'oracle_point rc={rc}')
     return out
+
+
+def validate_mt(problem_id, ops, offsets, prm=None, threads=None, chunk=64):
+    """validate() over a thread pool (the C oracle keeps no global state and ctypes releases
+    the GIL): chunks of `chunk` programs, results identical to the one-thread call."""
+    from concurrent.futures import ThreadPoolExecutor
+    lib = load()
+    ops = np.ascontiguousarray(ops, dtype=np.int32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    n = len(offsets) - 1
+    nref = 1 if problem_id == 0 else 3
+    out = dict(status=np.full(n, 255, np.uint8), q_ref=np.zeros(n), res_ref=np.zeros(n * nref),
+               q_grid=np.zeros(n), n_bad=np.zeros(n, np.int32), n_nonfinite=np.zeros(n, np.int32),
+               fingerprint=np.zeros(n * 4))
+    prm = prm or params()
+    ptrs = [out[k].ctypes.data for k in ('status', 'q_ref', 'res_ref', 'q_grid', 'n_bad',
+                                         'n_nonfinite', 'fingerprint')]
+
+    def run(first):
+        lib.oracle_validate(problem_id, ops.ctypes.data, offsets.ctypes.data, n, C.addressof(prm),
+                            *ptrs, first, min(chunk, n - first))
+    threads = threads or min(16, int(os.environ.get('OMP_NUM_THREADS', '0') or os.cpu_count() or 1))
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, range(0, n, chunk)))
+    out['res_ref'] = out['res_ref'].reshape(n, nref)
+    out['fingerprint'] = out['fingerprint'].reshape(n, 4)
+    return out
