@@ -108,6 +108,22 @@ enum pdeval_opcode {
 /* Immediate-carrying opcode word (PUSH_C, ADDC, MULC, RDIVC): bit 8 set = a double-double
    low part follows the f64 immediate (2 more words, low word first).                    */
 #define PDEVAL_IMM_DD     (1u << 8)
+/* bit 9 set (PUSH_C, ADDC, MULC, RDIVC; never with PDEVAL_IMM_DD) = the immediate is one of the
+   problem's constants (Kerr M, a), not a literal: the first word is a descriptor, bits 0-2 =
+   PDEVAL_PRM_* (M, a, 1/M, 1/a, M^2, a^2, 1/M^2, 1/a^2), bit 3 = negated; the second word is
+   0.  Its value is the
+   stage's: the point stage substitutes the validator's M_value / a_value, the constant test and
+   the grid stage the stand-ins of the symbols (pdeval_kerr_constants).                   */
+#define PDEVAL_IMM_PRM    (1u << 9)
+#define PDEVAL_PRM_M      0
+#define PDEVAL_PRM_A      1
+#define PDEVAL_PRM_INV_M  2
+#define PDEVAL_PRM_INV_A  3
+#define PDEVAL_PRM_M2     4   /* (index + 4: the square; index ^ 2: the reciprocal) */
+#define PDEVAL_PRM_A2     5
+#define PDEVAL_PRM_INV_M2 6
+#define PDEVAL_PRM_INV_A2 7
+#define PDEVAL_PRM_NEG    8
 
 /* Program header word: opcode 0 | stack depth << 8 | flags */
 #define PDEVAL_FLAG_COMPLEX  (1u << 16)  /* pushes the imaginary unit: complex pass only   */
@@ -167,6 +183,28 @@ typedef struct pdeval_ctx pdeval_ctx;
 int pdeval_create(int device_id, int problem_id, const double* grid, int n_grid, pdeval_ctx** out);
 int pdeval_destroy(pdeval_ctx* ctx);
 const char* pdeval_last_error(pdeval_ctx* ctx);
+
+/* Kerr constants (kerr_magnetosphere/validator.py:36-44, :69-91, :163-192).  The reference
+ * substitutes M = M_value, a = a_value only in its fast point check; its constant test
+ * (simplify(u) free of r and x, :231-240) and its symbolic stage (:283-300) keep M and a as the
+ * problem's symbols.  The device therefore evaluates the point stage at (M_value, a_value) and
+ * the constant test and the grid stage -- the symbolic stage's surrogate -- at (M_sym, a_sym),
+ * stand-ins for the symbols (generic values; a_sym < M_sym so that the horizon r+ exists).
+ * op_M_fixed / op_a_fixed: the validator was built with the NUMBER M_value (a_value) in place of
+ * the symbol (KerrMagnetosphereValidator(r, x, M, 0, ...)): the operator then uses that number
+ * in every stage, and u's own M (a) is a free symbol, evaluated at M_sym (a_sym) in every stage.
+ * pdeval_create uses the defaults (M_value = 1, a_value = 1/10, problems/__init__.py:283); the
+ * default grid follows r+ of the grid stage's operator (DESIGN.md "Grids").              */
+typedef struct pdeval_kerr_constants {
+    int64_t M_num, M_den;   /* M_value = M_num / M_den (|M_num|, M_den < 2^53)             */
+    int64_t a_num, a_den;   /* a_value                                                     */
+    double  M_sym, a_sym;   /* stand-ins for the symbols M and a                           */
+    int32_t op_M_fixed, op_a_fixed;
+} pdeval_kerr_constants;
+int pdeval_default_kerr_constants(pdeval_kerr_constants* out);
+/* Kerr contexts only; rebuilds the operator tables (and the default grid).  Not while a call
+ * on the context is in flight.                                                            */
+int pdeval_set_kerr_constants(pdeval_ctx* ctx, const pdeval_kerr_constants* k);
 
 int pdeval_n_ref_points(pdeval_ctx* ctx);
 int pdeval_n_points(pdeval_ctx* ctx);          /* n_ref + grid points */

@@ -139,6 +139,51 @@ static void w_horner(const double* h0, const double* F, double* out, int K) {
 #undef S
 #undef FN
 
+/* ---------------------------------------------------------------- Kerr constants
+ * The reference substitutes M = M_value, a = a_value in its fast point check only
+ * (kerr validator.py:163-192); its constant test (:231-240) and symbolic stage (:283-300) keep M
+ * and a symbolic.  Restated as in pdeval.h (pdeval_kerr_constants): the point stage at
+ * (M_value, a_value), the constant test and the grid at stand-ins of the symbols; a constant the
+ * validator was built with as a number (op_*_fixed) is that number in the operator of every
+ * stage, and u's own symbol is then free (its stand-in everywhere). */
+static struct {
+    __float128 opM_pt, opa_pt;      /* operator, point stage (exact rationals, quad) */
+    double opM_g, opa_g;            /* operator, grid stage */
+    double prm_pt[8], prm_g[8];     /* u's constants {M, a, 1/M, 1/a, M^2, a^2, 1/M^2, 1/a^2} */
+    __float128 prm_pt_q[8], prm_g_q[8];
+    int set;
+} KC;
+
+int oracle_set_kerr_constants(int64_t M_num, int64_t M_den, int64_t a_num, int64_t a_den, double M_sym,
+                              double a_sym, int op_M_fixed, int op_a_fixed) {
+    const __float128 Mq = (__float128)M_num / M_den, aq = (__float128)a_num / a_den;
+    KC.opM_pt = Mq;
+    KC.opa_pt = aq;
+    KC.opM_g = op_M_fixed ? (double)((long double)M_num / M_den) : M_sym;
+    KC.opa_g = op_a_fixed ? (double)((long double)a_num / a_den) : a_sym;
+    const __float128 uM = op_M_fixed ? (__float128)M_sym : Mq, ua = op_a_fixed ? (__float128)a_sym : aq;
+    const __float128 Mg = M_sym, ag = a_sym;
+    const __float128 pq[8] = {uM, ua, 1 / uM, 1 / ua, uM * uM, ua * ua, 1 / (uM * uM), 1 / (ua * ua)};
+    const __float128 gq[8] = {Mg, ag, 1 / Mg, 1 / ag, Mg * Mg, ag * ag, 1 / (Mg * Mg), 1 / (ag * ag)};
+    for (int k = 0; k < 8; ++k) {
+        KC.prm_pt_q[k] = pq[k];
+        KC.prm_g_q[k] = gq[k];
+        KC.prm_pt[k] = (double)pq[k];
+        KC.prm_g[k] = (double)gq[k];
+    }
+    KC.set = 1;
+    return 0;
+}
+
+static void kc_default(void) {
+    /* pdeval_default_kerr_constants: M_value = 1, a_value = 1/10 (problems/__init__.py:283) */
+    if (!KC.set) oracle_set_kerr_constants(1, 1, 1, 10, 1.171875, 0.359375, 0, 0);
+}
+
+/* the Kerr constant-test points (pdeval.hip build_points): the reference points, then two more */
+static const double kCtX[5] = {5.0 / 2.0, 7.0 / 3.0, 5.0, 3.3, 6.1};
+static const double kCtY[5] = {3.0 / 5.0, 1.0 / 3.0, -2.0 / 5.0, 0.27, -0.55};
+
 /* ---------------------------------------------------------------- sample points */
 /* Restates DESIGN.md "Grids" (the device builds the same table in pdeval_create). */
 static int build_points(int problem, double** px, double** py, int* n_ref) {
@@ -150,7 +195,9 @@ static int build_points(int problem, double** px, double** py, int* n_ref) {
         x_lo = 0.05; x_hi = 3.0;
         nr = 1; rx[0] = 4.0 / 5.0; ry[0] = 6.0 / 7.0;
     } else {
-        double rp = 1.0 + sqrt(1.0 - 0.01);
+        kc_default();
+        /* r+ = M + sqrt(M^2 - a^2) of the grid stage's operator */
+        double rp = KC.opM_g + sqrt(KC.opM_g * KC.opM_g - KC.opa_g * KC.opa_g);
         x_lo = rp + 0.1; x_hi = rp + 6.1; y_lo = -0.98; y_hi = 0.98;
         nr = 3;
         rx[0] = 5.0 / 2.0; ry[0] = 3.0 / 5.0;
@@ -170,12 +217,11 @@ static int build_points(int problem, double** px, double** py, int* n_ref) {
     return n;
 }
 
-/* Kerr linear surrogate at M = 1, a = 1/10, expanded by hand from kerr validator.py:77-91:
+/* Kerr linear surrogate at the operator's (M, a), expanded by hand from kerr validator.py:77-91:
  * d_r[G/(1-x^2) u_r] + d_x[G/Delta u_x]
  *   = G/(1-x^2) u_rr + G_r/(1-x^2) u_r + G/Delta u_xx + G_x/Delta u_x            */
 static void kerr_terms(double r, double x, const double complex* c, int cplx, double complex* L,
-                       double* scale) {
-    const double M = 1.0, a = 0.1;
+                       double* scale, double M, double a) {
     double s = r * r + a * a * x * x;
     double G = 1.0 - 2.0 * M * r / s;
     double Gr = -2.0 * M / s + 4.0 * M * r * r / (s * s);
@@ -201,17 +247,21 @@ typedef struct {
 #define NOISE_GAMMA 0x1p-30
 #define EPS64 0x1p-52
 
+/* grid: the constant test's / grid stage's constants (else the point stage's) */
 static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x, double y, int cplx,
-                            int tier2, int* rc) {
+                            int tier2, int* rc, int grid) {
     pt_result r = {0};
     const int K = problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
     double complex cc[NCMAX];
     double W[NCMAX];
+    kc_default();
+    const double* prm = grid ? KC.prm_g : KC.prm_pt;
+    const double opM = grid ? KC.opM_g : (double)KC.opM_pt, opa = grid ? KC.opa_g : (double)KC.opa_pt;
     if (cplx) {
-        *rc = run_c(w, nw, x, y, K, 1, cc, tier2 ? W : NULL, 0.0);
+        *rc = run_c(w, nw, x, y, K, 1, cc, tier2 ? W : NULL, 0.0, prm);
     } else {
         double cr[NCMAX];
-        *rc = run_r(w, nw, x, y, K, 0, cr, tier2 ? W : NULL, 0.0);
+        *rc = run_r(w, nw, x, y, K, 0, cr, tier2 ? W : NULL, 0.0, prm);
         for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
     }
     if (*rc) return r;
@@ -223,7 +273,7 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
         res = ff_det_c(cc, x, 0);
         r.scale = creal(ff_det_c(cc, x, 1));
     } else {
-        kerr_terms(x, y, cc, cplx, &res, &r.scale);
+        kerr_terms(x, y, cc, cplx, &res, &r.scale, opM, opa);
     }
     if (tier2) {
         double complex cp[NCMAX];
@@ -231,12 +281,18 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
         double S2;
         for (int i = 0; i < NC(K); ++i) cp[i] = cabs(cc[i]) + NOISE_GAMMA * W[i];
         if (problem == PDEVAL_PROBLEM_FORCE_FREE) S2 = creal(ff_det_c(cp, x, 1));
-        else kerr_terms(x, y, cp, 0, &res2, &S2);
+        else kerr_terms(x, y, cp, 0, &res2, &S2, opM, opa);
         r.noise = (S2 - r.scale) * (EPS64 / NOISE_GAMMA) + EPS64 * r.scale;
     }
     r.res_abs = cabs(res);
     r.res_re = creal(res);
     r.finite = fin && isfinite(creal(res)) && isfinite(cimag(res)) && isfinite(r.scale);
+    if (problem != PDEVAL_PROBLEM_FORCE_FREE) {
+        /* Kerr: a jet exactly 0 to second order is an underflow, not a sample (pdeval_kernels.h) */
+        int allz = 1;
+        for (int i = 0; i < NC(K); ++i) allz = allz && cc[i] == 0;
+        if (allz) r.finite = 0;
+    }
     r.grad_zero = cc[IDX(1, 0)] == 0 && cc[IDX(0, 1)] == 0;
     r.u0 = creal(cc[0]);
     return r;
@@ -258,7 +314,7 @@ static void ref_point_q(int problem, int k, __float128* x, __float128* y) {
 }
 
 static __complex128 kerr_lhs_q(__float128 r, __float128 x, const __complex128* c, double* scale) {
-    const __float128 M = 1, a = (__float128)1 / 10;
+    const __float128 M = KC.opM_pt, a = KC.opa_pt;   /* the point stage's operator */
     __float128 s = r * r + a * a * x * x;
     __float128 G = 1 - 2 * M * r / s;
     __float128 Gr = -2 * M / s + 4 * M * r * r / (s * s);
@@ -279,7 +335,8 @@ static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, 
     __complex128 cq[NCMAX];
     double W[NCMAX];
     /* the reference points are quad-rounded: 2^-113 relative, 1/32 of EPSQ */
-    *rc = run_q(w, nw, x, y, K, cplx, cq, W, 1.0 / 32);
+    kc_default();
+    *rc = run_q(w, nw, x, y, K, cplx, cq, W, 1.0 / 32, KC.prm_pt_q);
     if (*rc) return r;
     int fin = 1;
     double complex cd[NCMAX], cp[NCMAX];
@@ -297,7 +354,7 @@ static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, 
     } else {
         double complex dummy;
         res = kerr_lhs_q(x, y, cq, &r.scale);
-        kerr_terms((double)x, (double)y, cp, 0, &dummy, &S2);
+        kerr_terms((double)x, (double)y, cp, 0, &dummy, &S2, (double)KC.opM_pt, (double)KC.opa_pt);
     }
     r.noise = (S2 - r.scale) * (EPSQ / NOISE_GAMMA) + EPSQ * r.scale;
     r.res_abs = (double)cabsq(res);
@@ -310,6 +367,22 @@ static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, 
     r.grad_err[1] = W[IDX(0, 1)];
     r.u0 = (double)crealq(cq[0]);
     return r;
+}
+
+/* Kerr constant test at the stand-ins of the symbols (pdeval_point.h kerr_constant_test): at
+ * every constant-test point, u finite and its gradient within kappa x its rounding bound (quad) */
+static int kerr_constant_test(const int32_t* w, int64_t nw, double kappa) {
+    kc_default();
+    for (int p = 0; p < 5; ++p) {
+        __complex128 cq[NCMAX];
+        double W[NCMAX];
+        if (run_q(w, nw, (__float128)kCtX[p], (__float128)kCtY[p], 2, 0, cq, W, 0.0, KC.prm_g_q)) return 0;
+        for (int i = 0; i < NC(2); ++i)
+            if (!(fabsq(crealq(cq[i])) < 0x1p160Q)) return 0;
+        if ((double)cabsq(cq[IDX(1, 0)]) > kappa * (double)EPSQ * W[IDX(1, 0)]) return 0;
+        if ((double)cabsq(cq[IDX(0, 1)]) > kappa * (double)EPSQ * W[IDX(0, 1)]) return 0;
+    }
+    return 1;
 }
 
 /* Validate n programs; outputs as in pdeval_outputs (host arrays, any may be NULL).
@@ -341,7 +414,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
         qr = 0; qmax = 0; nb = nnf = nfin = any_grad = point_reject = 0; gconst = 1;
         for (int p = 0; p < npts && cls < 0; ++p) {
             int rc;
-            pt_result r = eval_point(problem, w, nw, px[p], py[p], cplx, 0, &rc);
+            pt_result r = eval_point(problem, w, nw, px[p], py[p], cplx, 0, &rc, p >= nref);
             if (rc == -2 || rc == -3) { cls = PDEVAL_CLS_UNSUPPORTED; break; }
             if (rc) { cls = PDEVAL_CLS_BAD_PROGRAM; break; }
             for (int f = 0; f < PDEVAL_FP_N; ++f)
@@ -394,16 +467,20 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
             nb = 0;
             for (int p = nref; p < npts; ++p) {
                 int rc2;
-                pt_result r2 = eval_point(problem, w, nw, px[p], py[p], cplx, 1, &rc2);
+                pt_result r2 = eval_point(problem, w, nw, px[p], py[p], cplx, 1, &rc2, 1);
                 if (rc2 || !r2.finite) continue;
                 if (scaled(r2.res_abs, r2.scale) > prm->tau_grid && r2.res_abs > prm->noise_kappa * r2.noise) ++nb;
             }
         }
         if (cls < 0) {
             int structural = problem != PDEVAL_PROBLEM_FORCE_FREE || (hdr & PDEVAL_FLAG_NOCOORD);
-            if (problem != PDEVAL_PROBLEM_FORCE_FREE && gconst) any_grad = 0;
-            if (!any_grad && nfin > 0 && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+            const int pconst = problem != PDEVAL_PROBLEM_FORCE_FREE && gconst &&
+                               kerr_constant_test(w, nw, prm->noise_kappa);
+            if (pconst) any_grad = 0;
+            if (!any_grad && (nfin > 0 || pconst) && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
             else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;
+            /* Kerr: no finite grid point proves nothing (the device's rule) */
+            else if (problem != PDEVAL_PROBLEM_FORCE_FREE && nfin == 0) cls = PDEVAL_CLS_REJECT_GRID;
             else if (nb > prm->max_bad) cls = PDEVAL_CLS_REJECT_GRID;
             else if (problem == PDEVAL_PROBLEM_FORCE_FREE && prm->strict_symbolic &&
                      (hdr & (PDEVAL_FLAG_NONSMOOTH2D | PDEVAL_FLAG_UNPROVABLE))) cls = PDEVAL_CLS_REJECT_SYMBOLIC;
@@ -427,10 +504,12 @@ int oracle_jet(int problem, const int32_t* w, int64_t nw, double x, double y, in
     double complex cc[NCMAX];
     int rc;
     if (cplx) {
-        rc = run_c(w, nw, x, y, K, 1, cc, NULL, 0.0);
+        kc_default();
+        rc = run_c(w, nw, x, y, K, 1, cc, NULL, 0.0, KC.prm_g);
     } else {
         double cr[NCMAX];
-        rc = run_r(w, nw, x, y, K, 0, cr, NULL, 0.0);
+        kc_default();
+        rc = run_r(w, nw, x, y, K, 0, cr, NULL, 0.0, KC.prm_g);
         for (int i = 0; i < NC(K); ++i) cc[i] = cr[i];
     }
     for (int i = 0; i < NC(K) && !rc; ++i) { re[i] = creal(cc[i]); im[i] = cimag(cc[i]); }
@@ -441,7 +520,7 @@ int oracle_jet(int problem, const int32_t* w, int64_t nw, double x, double y, in
  * threshold calibration). */
 int oracle_point(int problem, const int32_t* w, int64_t nw, double x, double y, int cplx, double* out) {
     int rc;
-    pt_result r = eval_point(problem, w, nw, x, y, cplx, 1, &rc);
+    pt_result r = eval_point(problem, w, nw, x, y, cplx, 1, &rc, 1);
     out[0] = r.res_abs;
     out[1] = r.scale;
     out[2] = r.noise;

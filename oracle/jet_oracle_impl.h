@@ -79,9 +79,10 @@ static void FN(wabs)(const S* v, double* w, int K) { for (int i = 0; i < NC(K); 
 
 /* Evaluate a program at (px, py).  eout != NULL: also carry the first-order rounding-error
  * jet E (rules at w_mul in jet_oracle.c) and return it. */
-/* cerr: relative rounding of the coordinates in noise units (0 on the exact grid points) */
+/* cerr: relative rounding of the coordinates in noise units (0 on the exact grid points);
+ * prm: the stage's values of the problem's constants {M, a, 1/M, 1/a} (PDEVAL_IMM_PRM) */
 static int FN(run)(const int32_t* w, int64_t nw, CT px, CT py, int K, int cplx_pass, S* out,
-                   double* eout, double cerr) {
+                   double* eout, double cerr, const CT* prm) {
     S st[16][NCMAX];
     double es[16][NCMAX];
     const int trk = eout != NULL;
@@ -89,7 +90,16 @@ static int FN(run)(const int32_t* w, int64_t nw, CT px, CT py, int K, int cplx_p
     for (int64_t pc = 1; pc < nw;) {
         uint32_t word = (uint32_t)w[pc], op = word & 0xffu;
         CT imm = 0;
-        if (op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC || op == PDOP_POW) {
+        if ((word & PDEVAL_IMM_PRM) && (op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC)) {
+            /* one of the problem's constants: descriptor word, then 0 */
+            if (pc + 2 >= nw || (word & PDEVAL_IMM_DD)) return -1;
+            const uint32_t dsc = (uint32_t)w[pc + 1];
+            if (dsc > 15u || w[pc + 2] != 0) return -1;
+            imm = prm[dsc & 7u];
+            if (dsc & PDEVAL_PRM_NEG) imm = -imm;
+            pc += 3;
+        } else if (op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC || op == PDOP_POW) {
+            if (word & PDEVAL_IMM_PRM) return -1;      /* (never an exponent) */
             const int nimm = (word & PDEVAL_IMM_DD) ? 2 : 1;
             if (pc + 2 * nimm >= nw + 1) return -1;
             for (int k = 0; k < nimm; ++k) {

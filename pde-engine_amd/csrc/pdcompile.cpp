@@ -104,12 +104,13 @@ struct SymInfo {
     const char* name;
     int coord;         // 0 = x (rho | r), 1 = y (z | x), -1 = constant
     bool positive;     // SymPy assumptions (problems/__init__.py:70-71, :263-266)
-    Rat value;         // constants: the value KerrMagnetosphereValidator substitutes
+    int prm;           // constants: the program parameter (PDEVAL_PRM_*) that stands for it; the
+                       // device gives it the stage's value (PDEVAL_IMM_PRM, pdeval.h)
 };
 
-const SymInfo kFFSyms[] = {{"rho", 0, true, {0, 1}}, {"z", 1, false, {0, 1}}};
-const SymInfo kKerrSyms[] = {{"r", 0, true, {0, 1}}, {"x", 1, false, {0, 1}},
-                             {"M", -1, true, {1, 1}}, {"a", -1, false, {1, 10}}};
+const SymInfo kFFSyms[] = {{"rho", 0, true, -1}, {"z", 1, false, -1}};
+const SymInfo kKerrSyms[] = {{"r", 0, true, -1}, {"x", 1, false, -1},
+                             {"M", -1, true, PDEVAL_PRM_M}, {"a", -1, false, PDEVAL_PRM_A}};
 
 // three-valued logic for SymPy's assumption queries
 enum Tri : int8_t { NO = 0, YES = 1, UNK = 2 };
@@ -803,6 +804,7 @@ struct IR {
     Rat r{0, 1};      // IC: exact value (rational constants)
     bool irr = false; // IC: irrational constant (E), flatten.py's ('c', v, e, False)
     Rat alpha;        // IPOW exact exponent (det_rational)
+    int prm = -1;     // IC: a constant of the problem (PDEVAL_PRM_*), kept symbolic
     int n = 0;        // IPOWN
     int a = -1, b = -1;
 };
@@ -847,6 +849,11 @@ struct Lower {
     }
     int pown(int b, int n) {
         if (n == 1) return b;
+        if (n == 2 && ir[b].k == IC && ir[b].prm >= 0 && ir[b].prm < 4) {   // M^2, a^2: a constant too
+            IR x{IC};
+            x.prm = ir[b].prm + PDEVAL_PRM_M2;
+            return mk(x);
+        }
         if (n <= 16) { IR x{IPOWN}; x.a = b; x.n = n; return mk(x); }
         IR x{IPOW}; x.a = b; x.c = (double)n; x.alpha = Rat{n, 1}; return mk(x);
     }
@@ -857,7 +864,9 @@ struct Lower {
                 const SymInfo& si = C.syms[nd.sym];
                 if (si.coord == 0) return mk(IR{IX});
                 if (si.coord == 1) return mk(IR{IY});
-                return cst(si.value);
+                IR x{IC};          // flatten.py ('m', k): rational in every stage (det_rational)
+                x.prm = si.prm;
+                return mk(x);
             }
             case NUM: return cst(nd.r);
             case ADD: return add(e);
@@ -981,7 +990,7 @@ struct Lower {
         if (i == j) return true;
         if (i < 0 || j < 0) return false;
         const IR &x = ir[i], &y = ir[j];
-        if (x.k != y.k || x.n != y.n || x.irr != y.irr || x.r.p != y.r.p || x.r.q != y.r.q ||
+        if (x.k != y.k || x.n != y.n || x.irr != y.irr || x.prm != y.prm || x.r.p != y.r.p || x.r.q != y.r.q ||
             x.alpha.p != y.alpha.p || x.alpha.q != y.alpha.q || !(x.c == y.c) || !(x.lo == y.lo))
             return false;
         return same(x.a, y.a) && same(x.b, y.b);
@@ -1123,18 +1132,32 @@ struct Emit {
         word64(imm);
         if (lo != 0.0) word64(lo);
     }
+    // an immediate that is the problem's constant: descriptor word (PDEVAL_PRM_* | NEG), then 0
+    void opp(int code, int desc) {
+        op(code, (int)(PDEVAL_IMM_PRM >> 8));
+        w.push_back(desc);
+        w.push_back(0);
+    }
     int parg(int i) const { return L.ir[i].n | ((L.ir[L.ir[i].a].k == IX ? 0 : 1) << 8); }
     void leaf(int i) {
         const IR& x = L.ir[i];
         if (L.is_pvar(i)) op(PDOP_PUSH_P, parg(i));
         else if (x.k == IX) op(PDOP_PUSH_X);
         else if (x.k == IY) op(PDOP_PUSH_Y);
+        else if (x.prm >= 0) opp(PDOP_PUSH_C, x.prm);
         else opi(PDOP_PUSH_C, x.c, x.lo);
     }
     void fused(IK k, int lf) {
         const IR& x = L.ir[lf];
         if (L.is_pvar(lf)) {
             op(k == IADD ? PDOP_ADD_P : k == ISUB ? PDOP_SUB_P : k == IMUL ? PDOP_MUL_P : PDOP_DIV_P, parg(lf));
+            return;
+        }
+        if (x.k == IC && x.prm >= 0) {
+            if (k == IADD) opp(PDOP_ADDC, x.prm);
+            else if (k == ISUB) opp(PDOP_ADDC, x.prm | PDEVAL_PRM_NEG);
+            else if (k == IMUL) opp(PDOP_MULC, x.prm);
+            else opp(PDOP_MULC, x.prm ^ PDEVAL_PRM_INV_M);   // / M = * (1/M)
             return;
         }
         if (x.k == IC) {
@@ -1174,6 +1197,7 @@ struct Emit {
         if (L.is_leaf(b)) { emit(a); fused(k, b); return; }
         if (L.is_leaf(a) && (k == IADD || k == IMUL)) { emit(b); fused(k, a); return; }
         if (L.is_leaf(a) && k == ISUB) { emit(b); op(PDOP_NEG); fused(IADD, a); return; }
+        if (k == IDIV && L.ir[a].k == IC && L.ir[a].prm >= 0) { emit(b); opp(PDOP_RDIVC, L.ir[a].prm); return; }
         if (k == IDIV && L.ir[a].k == IC) { emit(b); opi(PDOP_RDIVC, L.ir[a].c, L.ir[a].lo); return; }
         if (k == IDIV && L.is_pvar(a)) { emit(b); op(PDOP_RDIV_P, parg(a)); return; }
         const int na = L.need(a), nb = L.need(b);
@@ -1208,7 +1232,8 @@ int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t le
             if (o == PDOP_PUSH_Y || o == PDOP_ADD_Y || o == PDOP_SUB_Y || o == PDOP_MUL_Y || o == PDOP_DIV_Y) ys = true;
             if (is_p_op(o)) { if ((wd >> 16) & 1) ys = true; else xs = true; }
             if (o == PDOP_ABS) ab = true;
-            k += (o == PDOP_PUSH_C || o == PDOP_ADDC || o == PDOP_MULC || o == PDOP_RDIVC || o == PDOP_POW) ? 3 : 1;
+            const bool imm = o == PDOP_PUSH_C || o == PDOP_ADDC || o == PDOP_MULC || o == PDOP_RDIVC || o == PDOP_POW;
+            k += imm ? ((wd & PDEVAL_IMM_DD) ? 5 : 3) : 1;
         }
         uint32_t hdr = (uint32_t)(E.dmax << 8);
         if (!(xs || ys)) hdr |= PDEVAL_FLAG_NOCOORD;

@@ -46,6 +46,12 @@ enum {
     PD_N_LISTS = 15
 };
 
+namespace {
+struct Grid {
+    double x_lo, x_hi, nx, y_lo, y_hi, ny, x_ph, y_ph;
+};
+}  // namespace
+
 struct pdeval_ctx {
     int device = 0;
     int problem = 0;
@@ -59,6 +65,14 @@ struct pdeval_ctx {
     double* d_gx = nullptr;   // nx grid abscissae
     double* d_gy = nullptr;   // ny grid ordinates
     double* d_kc = nullptr;
+    Grid grid{};                         // as given, or the problem's default (grid_default)
+    bool grid_default = true;
+    // the problem's constants (Kerr M, a; pdeval_kerr_constants) and their per-stage tables
+    pdeval_kerr_constants kconst{};
+    PrmTab<double> prm_pt{}, prm_grid{};
+    PrmTab<dd> prm_pt_dd{}, prm_grid_dd{};
+    double ct_x[8] = {}, ct_y[8] = {};   // Kerr constant-test points
+    int n_ct = 0;
     // scratch: work lists and their counters
     int64_t cap = 0;
     // device work lists (capacity cap each) and their counters d_counts[L_*]
@@ -145,23 +159,19 @@ static thread_local std::string g_err;
 // ---------------------------------------------------------------------------- point tables
 namespace {
 
-struct Grid {
-    double x_lo, x_hi, nx, y_lo, y_hi, ny, x_ph, y_ph;
-};
-
-// DESIGN.md "Grids": cell-offset grids that avoid the coordinate singular sets exactly.
-Grid default_grid(int problem) {
+// DESIGN.md "Grids": cell-offset grids that avoid the coordinate singular sets exactly.  Kerr:
+// r from r+ + 0.1 to r+ + 6.1, r+ = M + sqrt(M^2 - a^2) of the grid stage's operator.
+Grid default_grid(int problem, double M = 1.0, double a = 0.1) {
     if (problem == PDEVAL_PROBLEM_FORCE_FREE)
         return {0.05, 3.0, 64, -2.0, 2.0, 64, 0.37, 0.41};
-    const double r_plus = 1.0 + std::sqrt(0.99);  // M + sqrt(M^2 - a^2), M = 1, a = 1/10
+    const double r_plus = M + std::sqrt(M * M - a * a);
     return {r_plus + 0.1, r_plus + 6.1, 64, -0.98, 0.98, 64, 0.37, 0.41};
 }
 
-// Kerr operator coefficients (kerr validator.py:69-91, M = 1, a = 1/10):
+// Kerr operator coefficients (kerr validator.py:69-91):
 // L[u] = G/(1-x^2) u_rr + G/Delta u_xx + d_r(G)/(1-x^2) u_r + d_x(G)/Delta u_x
 // in double-double at an exact rational point (the point stage's second tier)
-void kerr_coeffs_dd(dd r, dd x, dd* k) {
-    const dd M = dd_from(1.0), a = dd_ratio(1.0, 10.0);
+void kerr_coeffs_dd(dd r, dd x, dd M, dd a, dd* k) {
     const dd a2x2 = a * a * x * x;
     const dd s = r * r + a2x2;
     const dd s2 = s * s;
@@ -176,8 +186,8 @@ void kerr_coeffs_dd(dd r, dd x, dd* k) {
     k[3] = dd_div(Gx, D);
 }
 
-void kerr_coeffs(double r_, double x_, double* k) {
-    const long double M = 1.0L, a = 0.1L, r = r_, x = x_;
+void kerr_coeffs(double r_, double x_, long double M, long double a, double* k) {
+    const long double r = r_, x = x_;
     const long double s = r * r + a * a * x * x;
     const long double G = 1.0L - 2.0L * M * r / s;
     const long double Gr = 2.0L * M * (r * r - a * a * x * x) / (s * s);
@@ -191,6 +201,102 @@ void kerr_coeffs(double r_, double x_, double* k) {
 }
 
 }  // namespace
+
+// The stage tables of the problem's constants and every point table that depends on them: the
+// grid (the default Kerr grid follows r+ of the grid stage's operator), its reciprocal
+// abscissae, and (Kerr) the operator coefficients -- at the reference points with the point
+// stage's operator (fp64 table and double-double), on the grid with the grid stage's.
+static int build_points(pdeval_ctx* c) {
+    const bool kerr = c->problem == PDEVAL_PROBLEM_KERR;
+    long double opM_pt = 1.0L, opa_pt = 0.0L, opM_g = 1.0L, opa_g = 0.0L;
+    dd opM_pt_dd = dd_from(1.0), opa_pt_dd = dd_from(0.0);
+    if (kerr) {
+        const pdeval_kerr_constants& k = c->kconst;
+        const dd Mv = dd_ratio((double)k.M_num, (double)k.M_den), av = dd_ratio((double)k.a_num, (double)k.a_den);
+        const double Mvd = (double)k.M_num / (double)k.M_den, avd = (double)k.a_num / (double)k.a_den;
+        const long double Mvl = (long double)k.M_num / (long double)k.M_den;
+        const long double avl = (long double)k.a_num / (long double)k.a_den;
+        // the operator: the point stage at (M_value, a_value); the grid stage at the stand-ins,
+        // except for a constant the validator was built with as a number
+        opM_pt = Mvl;
+        opa_pt = avl;
+        opM_pt_dd = Mv;
+        opa_pt_dd = av;
+        opM_g = k.op_M_fixed ? Mvl : (long double)k.M_sym;
+        opa_g = k.op_a_fixed ? avl : (long double)k.a_sym;
+        // u's own M and a: the stage's values; a free symbol (op_*_fixed) is the stand-in
+        const double uM = k.op_M_fixed ? k.M_sym : Mvd, ua = k.op_a_fixed ? k.a_sym : avd;
+        const dd uMd = k.op_M_fixed ? dd_from(k.M_sym) : Mv, uad = k.op_a_fixed ? dd_from(k.a_sym) : av;
+        (void)uM;
+        (void)ua;
+        // {M, a, 1/M, 1/a, M^2, a^2, 1/M^2, 1/a^2} in double-double; the fp64 table is the
+        // rounded high parts
+        auto table = [](dd M, dd a, PrmTab<dd>& t, PrmTab<double>& d) {
+            const dd M2 = M * M, a2 = a * a;
+            t = PrmTab<dd>{{M, a, recip(M), recip(a), M2, a2, recip(M2), recip(a2)}};
+            for (int i = 0; i < 8; ++i) d.v[i] = t.v[i].hi + t.v[i].lo;
+        };
+        table(uMd, uad, c->prm_pt_dd, c->prm_pt);
+        table(dd_from(k.M_sym), dd_from(k.a_sym), c->prm_grid_dd, c->prm_grid);
+        // the constant test: the reference points and two more (pdeval_point.h)
+        c->n_ct = 0;
+        for (int p = 0; p < c->n_ref; ++p) {
+            c->ct_x[c->n_ct] = c->ref_x[p];
+            c->ct_y[c->n_ct++] = c->ref_y[p];
+        }
+        c->ct_x[c->n_ct] = 3.3;
+        c->ct_y[c->n_ct++] = 0.27;
+        c->ct_x[c->n_ct] = 6.1;
+        c->ct_y[c->n_ct++] = -0.55;
+        if (c->grid_default) c->grid = default_grid(c->problem, (double)opM_g, (double)opa_g);
+    }
+    const Grid& g = c->grid;
+    const int nx = c->nx, ny = c->ny;
+    std::vector<double> gx(nx), gy(ny);
+    for (int i = 0; i < nx; ++i) gx[i] = g.x_lo + (i + g.x_ph) * ((g.x_hi - g.x_lo) / nx);
+    for (int j = 0; j < ny; ++j) gy[j] = g.y_lo + (j + g.y_ph) * ((g.y_hi - g.y_lo) / ny);
+    std::vector<double> kc;
+    if (kerr) {
+        kc.resize(4 * (size_t)c->n_pts);
+        for (int p = 0; p < c->n_ref; ++p) {
+            kerr_coeffs(c->ref_x[p], c->ref_y[p], opM_pt, opa_pt, &kc[4 * p]);
+            kerr_coeffs_dd(c->ref_xd[p], c->ref_yd[p], opM_pt_dd, opa_pt_dd, &c->kc_ref[4 * p]);
+        }
+        for (int i = 0; i < nx; ++i)
+            for (int j = 0; j < ny; ++j)
+                kerr_coeffs(gx[i], gy[j], opM_g, opa_g, &kc[4 * (c->n_ref + (size_t)i * ny + j)]);
+    }
+    // d_gx holds the abscissae and then their reciprocals 1.0 / gx (correctly rounded, the
+    // value rcp() forms on the device): the grid pass reads 1/x with a scalar load
+    for (int i = 0; i < nx; ++i) gx.push_back(1.0 / gx[i]);
+    HIPCHK(c, hipMemcpy(c->d_gx, gx.data(), 2 * nx * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_gy, gy.data(), ny * sizeof(double), hipMemcpyHostToDevice));
+    if (kerr) HIPCHK(c, hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice));
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_default_kerr_constants(pdeval_kerr_constants* k) {
+    if (!k) return PDEVAL_ERR_ARG;
+    // problems/__init__.py:283: M_value = 1, a_value = 1/10.  Stand-ins of the symbols: dyadic
+    // (exact doubles), away from the small-integer ratios the op vocabulary builds
+    // (expression_operations.py), a < M
+    *k = pdeval_kerr_constants{1, 1, 1, 10, 1.171875, 0.359375, 0, 0};
+    return PDEVAL_OK;
+}
+
+extern "C" int pdeval_set_kerr_constants(pdeval_ctx* c, const pdeval_kerr_constants* k) {
+    if (!c || !k || c->problem != PDEVAL_PROBLEM_KERR || k->M_den <= 0 || k->a_den <= 0 || k->M_num <= 0 ||
+        !(k->M_sym > 0.0) || !(std::fabs(k->a_sym) < k->M_sym) || std::fabs((double)k->M_num) >= 0x1p53 ||
+        std::fabs((double)k->a_num) >= 0x1p53 || (double)k->M_den >= 0x1p53 || (double)k->a_den >= 0x1p53 ||
+        std::fabs((double)k->a_num / (double)k->a_den) >= (double)k->M_num / (double)k->M_den) {
+        if (c) c->err = "pdeval_set_kerr_constants: bad argument (Kerr context; M > 0, |a| < M, dens > 0)";
+        return PDEVAL_ERR_ARG;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->kconst = *k;
+    return build_points(c);
+}
 
 extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, int n_grid,
                              pdeval_ctx** out) {
@@ -211,15 +317,15 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     pdeval_ctx* c = new pdeval_ctx();
     c->device = device_id;
     c->problem = problem_id;
-    Grid g = default_grid(problem_id);
-    if (grid && n_grid >= 8) std::memcpy(&g, grid, sizeof(Grid));
-    const int nx = (int)g.nx, ny = (int)g.ny;
+    c->grid = default_grid(problem_id);
+    c->grid_default = !(grid && n_grid >= 8);
+    if (!c->grid_default) std::memcpy(&c->grid, grid, sizeof(Grid));
+    const int nx = (int)c->grid.nx, ny = (int)c->grid.ny;
     if (nx <= 0 || ny <= 0 || ny % 64 != 0 || nx * ny > (1 << 22)) {
         delete c;
         g_err = "pdeval_create: bad grid";
         return PDEVAL_ERR_ARG;
     }
-    std::vector<double> px, py;
     // the reference points as exact ratios (numerator, denominator)
     std::vector<std::pair<double, double>> rx, ry;
     if (problem_id == PDEVAL_PROBLEM_FORCE_FREE) {
@@ -237,29 +343,13 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
         c->ref_yd[k] = dd_ratio(ry[k].first, ry[k].second);
         c->ref_x[k] = rx[k].first / rx[k].second;
         c->ref_y[k] = ry[k].first / ry[k].second;
-        px.push_back(c->ref_x[k]);
-        py.push_back(c->ref_y[k]);
-        if (problem_id == PDEVAL_PROBLEM_KERR) kerr_coeffs_dd(c->ref_xd[k], c->ref_yd[k], &c->kc_ref[4 * k]);
     }
-    std::vector<double> gx(nx), gy(ny);
-    for (int i = 0; i < nx; ++i) gx[i] = g.x_lo + (i + g.x_ph) * ((g.x_hi - g.x_lo) / nx);
-    for (int j = 0; j < ny; ++j) gy[j] = g.y_lo + (j + g.y_ph) * ((g.y_hi - g.y_lo) / ny);
-    for (int i = 0; i < nx; ++i)
-        for (int j = 0; j < ny; ++j) {
-            px.push_back(gx[i]);
-            py.push_back(gy[j]);
-        }
     c->nx = nx;
     c->ny = ny;
-    c->n_pts = (int)px.size();
+    c->n_pts = c->n_ref + nx * ny;
     const int G = nx * ny;
     c->fp_pts[0] = 0;
     for (int f = 1; f < PDEVAL_FP_N; ++f) c->fp_pts[f] = c->n_ref + (int)((int64_t)G * f / PDEVAL_FP_N) + 7 % G;
-    std::vector<double> kc;
-    if (problem_id == PDEVAL_PROBLEM_KERR) {
-        kc.resize(4 * px.size());
-        for (size_t p = 0; p < px.size(); ++p) kerr_coeffs(px[p], py[p], &kc[4 * p]);
-    }
     auto fail = [&](const char* what, hipError_t e) {
         g_err = std::string(what) + ": " + hipGetErrorString(e);
         pdeval_destroy(c);
@@ -270,19 +360,16 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_SORT")) c->sort = atoi(v) != 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
-    // d_gx holds the abscissae and then their reciprocals 1.0 / gx (correctly rounded, the
-    // value rcp() forms on the device): the grid pass reads 1/x with a scalar load
-    for (int i = 0; i < nx; ++i) gx.push_back(1.0 / gx[i]);
     if ((e = hipMalloc(&c->d_gx, 2 * nx * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc(&c->d_gy, ny * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
-    if ((e = hipMemcpy(c->d_gx, gx.data(), 2 * nx * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail("hipMemcpy", e);
-    if ((e = hipMemcpy(c->d_gy, gy.data(), ny * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
-        return fail("hipMemcpy", e);
-    if (!kc.empty()) {
-        if ((e = hipMalloc(&c->d_kc, kc.size() * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
-        if ((e = hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess)
-            return fail("hipMemcpy", e);
+    if (problem_id == PDEVAL_PROBLEM_KERR &&
+        (e = hipMalloc(&c->d_kc, 4 * (size_t)c->n_pts * sizeof(double))) != hipSuccess)
+        return fail("hipMalloc", e);
+    if (problem_id == PDEVAL_PROBLEM_KERR) pdeval_default_kerr_constants(&c->kconst);
+    if (int rc = build_points(c)) {
+        g_err = c->err;
+        pdeval_destroy(c);
+        return rc;
     }
     if ((e = hipMalloc(&c->d_counts, PD_N_LISTS * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
     *out = c;
@@ -372,6 +459,10 @@ extern "C" int pdeval_program_depth(const int32_t* ops, int64_t n_words) {
             const int n = (ops[pc] >> 8) & 0xff;
             if (n < 2 || n > 16) return -5;
         }
+        if (op_has_imm(op) && ((uint32_t)ops[pc] & PDEVAL_IMM_PRM)) {   // a constant of the problem
+            if (op == PDOP_POW || ((uint32_t)ops[pc] & PDEVAL_IMM_DD)) return -9;
+            if (pc + 2 < n_words && ((uint32_t)ops[pc + 1] > 15u || ops[pc + 2] != 0)) return -9;
+        }
         d += delta;
         if (d > dmax) dmax = d;
         pc += op_words(ops[pc]);
@@ -426,6 +517,18 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
 }
 
 // ---------------------------------------------------------------------------- launches
+static void copy_constants(const pdeval_ctx* c, KernelArgs& a) {
+    a.prm_pt = c->prm_pt;
+    a.prm_grid = c->prm_grid;
+    a.prm_pt_dd = c->prm_pt_dd;
+    a.prm_grid_dd = c->prm_grid_dd;
+    a.n_ct = c->n_ct;
+    for (int k = 0; k < 8; ++k) {
+        a.ct_x[k] = c->ct_x[k];
+        a.ct_y[k] = c->ct_y[k];
+    }
+}
+
 static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (n <= c->cap) return PDEVAL_OK;
     for (int64_t*& l : c->d_list) {
@@ -498,6 +601,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         a.ref_yd[k] = c->ref_yd[k];
     }
     for (int k = 0; k < 16; ++k) a.kc_ref[k] = c->kc_ref[k];
+    copy_constants(c, a);
     a.gx = c->d_gx;
     a.gy = c->d_gy;
     a.nx = c->nx;
@@ -896,6 +1000,7 @@ extern "C" int pdeval_point_eval(pdeval_ctx* c, const int32_t* prog, int64_t n_w
         a.ref_yd[k] = c->ref_yd[k];
     }
     for (int k = 0; k < 16; ++k) a.kc_ref[k] = c->kc_ref[k];
+    copy_constants(c, a);
     a.kc = c->d_kc;
     a.n_ref = c->n_ref;
     a.prm = prm;

@@ -62,6 +62,10 @@ template <int MAXD> __device__ __forceinline__ bool lean_prescan(const int32_t* 
         if (pc + len > plen) return false;
         // POWN beyond 8 takes the generic kernel (see pown_lean; none in the depth-4 streams)
         if (op == PDOP_POWN && ((w >> 8) & 0xffu) > 8u) return false;
+        // a constant of the problem (PDEVAL_IMM_PRM): a valid descriptor, never an exponent
+        if ((kImmMask & b) && (w & PDEVAL_IMM_PRM) &&
+            (op == PDOP_POW || (w & PDEVAL_IMM_DD) || rd_word(prog + pc + 1) > 15u))
+            return false;
         if (kPushMask & b) {
             if (++d > MAXD) return false;
         } else if (kBinMask & b) {
@@ -106,7 +110,7 @@ template <int K, int W, int MAXD> struct Lean {
     // forms them).  x[] is wave-uniform (one grid row each), y is the lane's ordinate.
     static __device__ __forceinline__ void run(const int32_t* prog, int plen, const double (&x)[W], double y,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
-                                               double* stk, int lane) {
+                                               double* stk, int lane, const PrmTab<double>& P) {
         int pc = 1;
         uint32_t w = rd_word(prog + 1);
         bool first = true;
@@ -148,20 +152,20 @@ template <int K, int W, int MAXD> struct Lean {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
                 } else {
-                    const double c = rd_imm(prog + pc + 1);
+                    const double c = rd_immp(prog + pc + 1, w, P);
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_const(acc[q], c);
                 }
             } else if (b & kCheapMask) {
                 if (op == PDOP_ADDC) {
-                    const double c = rd_imm(prog + pc + 1);
+                    const double c = rd_immp(prog + pc + 1, w, P);
 #pragma unroll
                     for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
                 } else if (op == PDOP_NEG) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], -1.0);
                 } else if (op == PDOP_MULC) {
-                    const double c = rd_imm(prog + pc + 1);
+                    const double c = rd_immp(prog + pc + 1, w, P);
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], c);
                 } else if (op == PDOP_ADD_X) {
@@ -232,7 +236,7 @@ template <int K, int W, int MAXD> struct Lean {
                 for (int q = 0; q < W; ++q) {
                     if (op == PDOP_EXP) O::expj(acc[q]);
                     else if (op == PDOP_POW) O::powa(acc[q], rd_imm(prog + pc + 1));
-                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], rd_imm(prog + pc + 1));
+                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], rd_immp(prog + pc + 1, w, P));
                     else if (op == PDOP_SQRT) O::sqrtj(acc[q]);
                     else if (op == PDOP_LOG) O::logj(acc[q]);
                     else if (op == PDOP_POWN) pown_lean(acc[q], pn);
@@ -288,12 +292,17 @@ template <int K, int W, int MAXD> struct Lean {
 // validate_kernel's epilogue, whose logic it restates for the point-decided case).
 __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, uint32_t hdr, int prob,
                                             bool point_reject, double qmax, int nbad, int nfin,
-                                            int nnonfin, bool any_grad) {
+                                            int nnonfin, bool any_grad, bool pconst) {
     int cls;
     uint32_t esc = 0;
     const bool structural = (prob != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);
-    if (!any_grad && nfin > 0 && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+    // (P0_CONST: the Kerr constant test passed -- also for u == 0, whose grid jets are all 0)
+    if (!any_grad && (nfin > 0 || pconst) && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
     else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;   // decided by the point stage: final
+    // Kerr: no finite grid point (u not real, or underflowed, everywhere on the grid at the
+    // stand-ins of the symbols): nothing proves lhs == 0 -- the reference's symbolic stage does
+    // not prove these either (kerr validator.py:283-315).  Final, no tier 2.
+    else if (prob != PDEVAL_PROBLEM_FORCE_FREE && nfin == 0) cls = PDEVAL_CLS_REJECT_GRID;
     else if (nbad > a.prm.max_bad) {
         cls = PDEVAL_CLS_REJECT_GRID;
         esc = ESC_GRID_EVAL | ESC_GRID_FAIL;
@@ -429,7 +438,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             constexpr bool kv_late = W > 2 || (MAXD == 2 && PD_KV_LATE) || (MAXD > 2 && PD_KV_LATE_DEEP);
             if constexpr (!kv_late) load_kv();
             J u[W];
-            L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane);
+            L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane, a.prm_grid);
             if constexpr (kv_late) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {
@@ -458,7 +467,8 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     qmax = wave_max(qmax);
     const bool any_grad = __any(grad_nz) && !(ps & P0_CONST);
     if (lane == 0)
-        grid_finish(a, cand, hdr, PROB, (ps & 3) == P0_REJECT, qmax, nbad, nfin, a.nx * a.ny - nfin, any_grad);
+        grid_finish(a, cand, hdr, PROB, (ps & 3) == P0_REJECT, qmax, nbad, nfin, a.nx * a.ny - nfin, any_grad,
+                    (ps & P0_CONST) != 0);
 }
 
 // pass 1: one wave per candidate, 4 per 256-thread block; a.defer_list takes stack-3+ programs,

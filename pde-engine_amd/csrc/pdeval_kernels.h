@@ -22,6 +22,21 @@
 
 namespace pd {
 
+// The problem's constants for one stage (Kerr M and a, PDEVAL_IMM_PRM): {M, a, 1/M, 1/a, M^2,
+// a^2, 1/M^2, 1/a^2} as the coordinate type V (double, or dd in the double-double point tier).  The point stage gets the
+// validator's M_value, a_value; the constant test and the grid stage the stand-ins of the
+// symbols (pdeval_kerr_constants).  Passed by value: 4 wave-uniform values, scalar selects.
+template <class V> struct PrmTab {
+    V v[8];
+};
+template <class V> PD_HD V prm_value(const PrmTab<V>& t, uint32_t d) {
+    const uint32_t k = d & 7u;
+    const V lo = (k & 1u) ? ((k & 2u) ? t.v[3] : t.v[1]) : ((k & 2u) ? t.v[2] : t.v[0]);
+    const V hi = (k & 1u) ? ((k & 2u) ? t.v[7] : t.v[5]) : ((k & 2u) ? t.v[6] : t.v[4]);
+    const V v = (k & 4u) ? hi : lo;
+    return (d & PDEVAL_PRM_NEG) ? -v : v;
+}
+
 struct KernelArgs {
     const int32_t* ops;
     const int64_t* offsets;
@@ -57,6 +72,13 @@ struct KernelArgs {
     double* noise_ref;          // n * n_ref fp64 noise bounds at the reference points (point stage)
     struct T2Acc* t2acc;        // tier 2: one accumulator per list entry (pdeval_tier2.h), zeroed
     const int32_t* perm;        // order of pass 0 and the tier-B collect pass (pdeval_sort.hip), or NULL
+    // the problem's constants per stage (PDEVAL_IMM_PRM; Kerr M, a): point stage (fp64 and
+    // double-double) and the constant test / grid stage
+    PrmTab<double> prm_pt, prm_grid;
+    PrmTab<dd> prm_pt_dd, prm_grid_dd;
+    // Kerr constant test (pdeval_point.h): points where u's gradient must be rounding noise
+    double ct_x[8], ct_y[8];
+    int n_ct;
 };
 
 // Partial grid counts of one tier-2 list entry whose grid is split over several waves.
@@ -136,6 +158,11 @@ __device__ __forceinline__ double rd_sf64(const double* p) {
 #else
     return *p;
 #endif
+}
+// an immediate that may be one of the problem's constants (PDEVAL_IMM_PRM)
+__device__ __forceinline__ double rd_immp(const int32_t* p, uint32_t w, const PrmTab<double>& P) {
+    if (w & PDEVAL_IMM_PRM) return prm_value(P, rd_word(p));
+    return rd_imm(p);
 }
 __device__ __forceinline__ bool op_has_imm(uint32_t op) {
     return op == PDOP_PUSH_C || op == PDOP_ADDC || op == PDOP_MULC || op == PDOP_RDIVC ||
@@ -615,9 +642,16 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue(const T*
     }
     r.grad_zero = is_zero(u[ji(1, 0)]) && is_zero(u[ji(0, 1)]);
     bool fin = finite_(L) && isfinite(r.scale);
+    // a jet that is exactly 0 to second order carries no information: u underflowed there
+    // (exp_neg(E*exp(r**2)*..) is 0 in fp64 on most of the grid), as an analytic u that is not
+    // identically 0 cannot vanish with its derivatives at a sample point
+    bool allz = true;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) fin = fin && jet_coef_ok(u[i]);
-    r.finite = fin;
+    for (int i = 0; i < 6; ++i) {
+        fin = fin && jet_coef_ok(u[i]);
+        allz = allz && is_zero(u[i]);
+    }
+    r.finite = fin && !allz;
     return r;
 }
 
@@ -692,7 +726,7 @@ template <class T, int K, int MAXD> struct Interp {
 
     // Evaluate program words [pc, end) at point (x, y); result jet in T.
     static __device__ __forceinline__ int run(const int32_t* ops, int pc, int end, double x, double y,
-                                              J& acc, T* stk, int lane) {
+                                              J& acc, T* stk, int lane, const PrmTab<double>& P) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
         uint32_t w = rd_word(ops + pc);
@@ -705,7 +739,7 @@ template <class T, int K, int MAXD> struct Interp {
             if (op_has_imm(op)) {
                 npc = pc + ((w & PDEVAL_IMM_DD) ? 5 : 3);   // (the double-double low part is skipped)
                 if (npc > end) return RUN_BAD;
-                imm = rd_imm(ops + pc + 1);
+                imm = rd_immp(ops + pc + 1, w, P);
             }
             const uint32_t wn = (npc < end) ? rd_word(ops + npc) : 0u;
             switch (op) {
@@ -918,7 +952,7 @@ void validate_kernel(KernelArgs a) {
             }
             const int pp = p;
             J u;
-            const int rc = I::run(prog, 1, plen, x, y, u, stk, lane);
+            const int rc = I::run(prog, 1, plen, x, y, u, stk, lane, ch == 0 ? a.prm_pt : a.prm_grid);
             if (rc == RUN_UNSUPPORTED) { status = PDEVAL_CLS_UNSUPPORTED; break; }
             if (rc == RUN_BAD) { status = PDEVAL_CLS_BAD_PROGRAM; break; }
             PointResult r;
@@ -996,7 +1030,9 @@ void validate_kernel(KernelArgs a) {
                 // u that simplify() reduces to a constant (kerr validator.py:231-240).
                 const bool structural = (PROB != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);
                 uint32_t esc = 0;
-                if (!any_grad && nfin > 0 && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+                if (!any_grad && (nfin > 0 || (ps & P0_CONST)) && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+                else if (PROB != PDEVAL_PROBLEM_FORCE_FREE && !point_reject && grid_eval && nfin == 0)
+                    cls = PDEVAL_CLS_REJECT_GRID;   // no finite grid point: nothing proves lhs == 0
                 else if (point_reject) {
                     cls = PDEVAL_CLS_REJECT_POINT;
                     if (!point_final)

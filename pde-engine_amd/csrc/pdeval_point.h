@@ -51,6 +51,15 @@ template <> __device__ __forceinline__ dd ref_coord<dd>(const KernelArgs& a, int
     return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3]));
 }
 
+// the problem's constants of the point stage (grid = false) or of the constant test / grid stage
+template <class V> __device__ __forceinline__ const PrmTab<V>& stage_prm(const KernelArgs& a, bool grid);
+template <> __device__ __forceinline__ const PrmTab<double>& stage_prm<double>(const KernelArgs& a, bool grid) {
+    return grid ? a.prm_grid : a.prm_pt;
+}
+template <> __device__ __forceinline__ const PrmTab<dd>& stage_prm<dd>(const KernelArgs& a, bool grid) {
+    return grid ? a.prm_grid_dd : a.prm_pt_dd;
+}
+
 struct PtEval {
     double res_re, res_im, res_abs;  // residual (hi parts)
     double S, noise;                 // magnitude scale and first-order noise bound
@@ -84,7 +93,7 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
     // the reference points are rounded to the coordinate type: half a unit of fp64, ~2^-7 of the
     // double-double noise unit (dd_unit = 2^-100 against a rounding of 2^-107)
     const double cerr = std::is_same<V, dd>::value ? 0x1p-6 : 0.5;
-    r.rc = EI::template run_s<VEC>(prog, 1, plen, x, y, u, e, stk, cerr);
+    r.rc = EI::template run_s<VEC>(prog, 1, plen, x, y, u, e, stk, stage_prm<V>(a, false), cerr);
     if (r.rc != RUN_OK) return r;
     double m[NC];
 #pragma unroll
@@ -113,6 +122,37 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
     for (int i = 0; i < NC; ++i) fin = fin && m[i] < kHugeJet;
     r.finite = fin;
     return r;
+}
+
+// Kerr constant test at the stand-ins of the symbols (kerr validator.py:231-240: u is dropped
+// when simplify(u), with M and a symbolic, has neither r nor x).  Run only for candidates whose
+// gradient is rounding noise at every reference point in the point stage's constants: then at
+// every constant-test point (the reference points and two more, so that a u merely stationary
+// at the reference points is not taken for a constant) with the grid stage's constants, the
+// gradient must lie within kappa x its first-order rounding bound.
+template <int PROB, class T, class V, int MAXD, bool VEC, class STK>
+__device__ __forceinline__ bool kerr_constant_test(const KernelArgs& a, const int32_t* prog, int plen, STK& stk) {
+    constexpr int K = 2;
+    constexpr int NC = nc(K);
+    using EI = ErrInterp<T, K, MAXD, V>;
+    const double unit = std::is_same<V, dd>::value ? dd_unit() / kEps : 1.0;
+    const double gk = a.prm.noise_kappa * kEps * unit;
+    for (int p = 0; p < a.n_ct && p < 8; ++p) {
+        typename EI::J u;
+        double e[NC];
+        const V x = cvt<V>(a.ct_x[p]), y = cvt<V>(a.ct_y[p]);
+        if (EI::template run_s<VEC>(prog, 1, plen, x, y, u, e, stk, stage_prm<V>(a, true), 0.0) != RUN_OK)
+            return false;
+        double m[NC];
+        bool fin = true;
+#pragma unroll
+        for (int i = 0; i < NC; ++i) {
+            m[i] = mag(u.c[i]);
+            fin = fin && m[i] < kHugeJet;
+        }
+        if (!fin || m[ji(1, 0)] > gk * e[ji(1, 0)] || m[ji(0, 1)] > gk * e[ji(0, 1)]) return false;
+    }
+    return true;
 }
 
 // ---- decision rules.  FINAL = the double-double tier (nothing is left undecided).
@@ -197,7 +237,9 @@ __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand
     else ps = und ? (uint8_t)(P0_DD | P0_PASS) : (rej ? P0_REJECT : P0_PASS);
     if (inacc) ps |= P0_DD;
     if (grad) ps |= P0_GRAD;
-    if (PROB != PDEVAL_PROBLEM_FORCE_FREE && gconst) ps |= P0_CONST;
+    if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
+        if (gconst && kerr_constant_test<PROB, T, V, MAXD, VEC>(a, prog, plen, stk)) ps |= P0_CONST;
+    }
     return ps;
 }
 
@@ -371,7 +413,8 @@ template <class T, int K, int MAXD, class V> struct ValInterp {
     using O = JetOps<T, K>;
     using J = typename O::J;
     template <class STK>
-    static __device__ int run(const int32_t* ops, int pc, int end, V x, V y, J& acc, STK& stk) {
+    static __device__ int run(const int32_t* ops, int pc, int end, V x, V y, J& acc, STK& stk,
+                              const PrmTab<V>& P) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
         for (;;) {
@@ -382,7 +425,7 @@ template <class T, int K, int MAXD, class V> struct ValInterp {
             if (op_has_imm(op)) {
                 npc = pc + ((w & PDEVAL_IMM_DD) ? 5 : 3);
                 if (npc > end) return RUN_BAD;
-                immv = read_imm<V, true>(ops + pc + 1, w);
+                immv = read_imm<V, true>(ops + pc + 1, w, P);
             }
             switch (op) {
                 case PDOP_PUSH_X: case PDOP_PUSH_Y: case PDOP_PUSH_C: case PDOP_PUSH_I:
@@ -467,7 +510,7 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
     for (int p = 0; p < a.n_ref; ++p) {
         const dd x = a.ref_xd[p & 3], y = a.ref_yd[p & 3];
         typename ValInterp<T, K, MAXD, dd>::J u;
-        if (ValInterp<T, K, MAXD, dd>::run(prog, 1, plen, x, y, u, stk) != RUN_OK) return P0_NONE;
+        if (ValInterp<T, K, MAXD, dd>::run(prog, 1, plen, x, y, u, stk, a.prm_pt_dd) != RUN_OK) return P0_NONE;
         double m[NC];
 #pragma unroll
         for (int i = 0; i < NC; ++i) m[i] = mag(u.c[i]);
@@ -499,7 +542,10 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
             rej = rej || kerr_point_rule<true>(res_abs, noise, a.prm) == 1;
         }
     }
-    if (!fin_all) return P0_NONE;
+    // Kerr: a reference point where even the double-double value is not finite is a pole (or
+    // a value beyond fp64): the reference's N(., 40) is zoo / nan / a float overflow there, a
+    // reject either way (kerr validator.py:178-190).  Force-free keeps the fp64 decision.
+    if (!fin_all) return PROB == PDEVAL_PROBLEM_FORCE_FREE ? P0_NONE : P0_REJECT;
     if (a.out.q_ref) a.out.q_ref[cand] = qr;
     if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) return ff & 3;
     else return rej ? P0_REJECT : P0_PASS;

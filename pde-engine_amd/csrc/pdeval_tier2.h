@@ -134,7 +134,12 @@ template <class T, int NC, int SLOTS> struct PrivStack {
 
 // Immediate of an opcode as the coordinate type V: the f64 word pair, plus the double-double
 // low part when the opcode carries PDEVAL_IMM_DD and V = dd.
-template <class V, bool VEC> __device__ __forceinline__ V read_imm(const int32_t* p, uint32_t w) {
+template <class V, bool VEC> __device__ __forceinline__ V read_imm(const int32_t* p, uint32_t w,
+                                                                  const PrmTab<V>& P) {
+    if (w & PDEVAL_IMM_PRM) {   // one of the problem's constants: the stage's value
+        if constexpr (VEC) return prm_value(P, (uint32_t)p[0]);
+        else return prm_value(P, rd_word(p));
+    }
     double hi, lo = 0.0;
     if constexpr (VEC) {
         hi = __hiloint2double(p[1], p[0]);
@@ -207,7 +212,7 @@ template <class T, int K, int MAXD, class V = double> struct ErrInterp {
     // their rounding is amplified like any other error)
     template <bool VEC, class STK>
     static __device__ int run_s(const int32_t* ops, int pc, int end, V x, V y, J& acc, double* ea, STK& stk,
-                                double cerr = 0.0) {
+                                const PrmTab<V>& P, double cerr = 0.0) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
         for (;;) {
@@ -221,7 +226,7 @@ template <class T, int K, int MAXD, class V = double> struct ErrInterp {
             if (op_has_imm(op)) {
                 npc = pc + ((w & PDEVAL_IMM_DD) ? 5 : 3);
                 if (npc > end) return RUN_BAD;
-                immv = read_imm<V, VEC>(ops + pc + 1, w);
+                immv = read_imm<V, VEC>(ops + pc + 1, w, P);
                 imm = hi_of(immv);
             }
             double A[NC], B[NC], R[NC];
@@ -412,9 +417,9 @@ template <class T, int K, int MAXD, class V = double> struct ErrInterp {
     // the LDS-stack form used by the tier-2 and diagnostic kernels
     template <bool VEC = false>
     static __device__ int run(const int32_t* ops, int pc, int end, V x, V y, J& acc, double* ea, T* vs,
-                              double* es, int lane) {
+                              double* es, int lane, const PrmTab<V>& P) {
         LdsStack<T, NC> stk{vs, es, lane};
-        return run_s<VEC>(ops, pc, end, x, y, acc, ea, stk);
+        return run_s<VEC>(ops, pc, end, x, y, acc, ea, stk, P);
     }
 };
 
@@ -489,7 +494,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             const double y = l == 0 ? a.ref_y[0] : (l == 1 ? a.ref_y[1] : (l == 2 ? a.ref_y[2] : a.ref_y[3]));
             J u;
             double e[NC];
-            const int rc = I::template run_s<false>(prog, 1, plen, x, y, u, e, stk);
+            const int rc = I::template run_s<false>(prog, 1, plen, x, y, u, e, stk, a.prm_pt);
             bool real_fail = rc != RUN_OK;
             if (rc == RUN_OK) {
                 const double* kc = a.kc ? a.kc + 4 * l : nullptr;
@@ -522,7 +527,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
                 const double y = a.gy[sl * 64 + lane];
                 J u;
                 double e[NC];
-                const int rc = I::template run_s<false>(prog, 1, plen, x, y, u, e, stk);
+                const int rc = I::template run_s<false>(prog, 1, plen, x, y, u, e, stk, a.prm_grid);
                 if (rc != RUN_OK) { ++nnonfin; continue; }
                 const double* kc = a.kc ? a.kc + 4 * p : nullptr;
                 PointResult r;
@@ -583,7 +588,8 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             const bool has_fin = eval_grid ? nfin > 0 : (flags & ESC_NFIN) != 0;
             const bool structural = (PROB != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);
             int cls;
-            if (!any_grad && has_fin && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+            if (!any_grad && (has_fin || pconst) && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
+            else if (PROB != PDEVAL_PROBLEM_FORCE_FREE && !has_fin) cls = PDEVAL_CLS_REJECT_GRID;
             else if (nbad_out > a.prm.max_bad) cls = PDEVAL_CLS_REJECT_GRID;
             else if (PROB == PDEVAL_PROBLEM_FORCE_FREE && a.prm.strict_symbolic && (hdr & (PDEVAL_FLAG_NONSMOOTH2D | PDEVAL_FLAG_UNPROVABLE)))
                 cls = PDEVAL_CLS_REJECT_SYMBOLIC;
@@ -631,8 +637,9 @@ __global__ __launch_bounds__(64, 1) void eval_points_kernel(const int32_t* prog,
     double e[NC];
 #pragma unroll
     for (int i = 0; i < NC; ++i) e[i] = 0.0;
-    const int rc = tier2 ? EI::template run<false>(prog, 1, plen, x, y, u, e, vs, es, lane)
-                         : I::run(prog, 1, plen, x, y, u, vs, lane);
+    const PrmTab<double> P{};   // (force-free: no constants of the problem)
+    const int rc = tier2 ? EI::template run<false>(prog, 1, plen, x, y, u, e, vs, es, lane, P)
+                         : I::run(prog, 1, plen, x, y, u, vs, lane, P);
     PointResult r;
     const double* k4 = kc ? kc + 4 * pc : nullptr;
     if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);

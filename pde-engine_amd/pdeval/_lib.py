@@ -25,6 +25,7 @@ EXPORTS = (
     'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts', 'pdeval_eval_points',
     'pdeval_compile_batch', 'pdeval_canonical', 'pdeval_point_eval', 'pdeval_point_states',
     'pdeval_comm_unique_id', 'pdeval_comm_init', 'pdeval_gather_bits', 'pdeval_comm_destroy',
+    'pdeval_default_kerr_constants', 'pdeval_set_kerr_constants',
 )
 MAX_BATCH = 1 << 30          # PDEVAL_MAX_BATCH
 UNIQUE_ID_BYTES = 128
@@ -46,6 +47,17 @@ class Outputs(C.Structure):
     _fields_ = [('verdict_bits', C.c_void_p), ('status', C.c_void_p), ('q_ref', C.c_void_p),
                 ('res_ref', C.c_void_p), ('q_grid', C.c_void_p), ('n_bad', C.c_void_p),
                 ('n_nonfinite', C.c_void_p), ('fingerprint', C.c_void_p)]
+
+
+class KerrConstants(C.Structure):
+    """pdeval_kerr_constants (include/pdeval.h): the validator's M_value, a_value (exact
+    rationals, the point stage) and the stand-ins of the symbols M, a (constant test, grid)."""
+    _fields_ = [('M_num', C.c_int64), ('M_den', C.c_int64), ('a_num', C.c_int64), ('a_den', C.c_int64),
+                ('M_sym', C.c_double), ('a_sym', C.c_double), ('op_M_fixed', C.c_int32),
+                ('op_a_fixed', C.c_int32)]
+
+    def key(self):
+        return tuple(getattr(self, f) for f, _ in self._fields_)
 
 
 class PdevalError(RuntimeError):
@@ -91,6 +103,8 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_comm_init.argtypes = [vp, C.c_int, C.c_int, vp]
     lib.pdeval_gather_bits.argtypes = [vp, vp, i64, vp, vp]
     lib.pdeval_comm_destroy.argtypes = [vp]
+    lib.pdeval_default_kerr_constants.argtypes = [C.POINTER(KerrConstants)]
+    lib.pdeval_set_kerr_constants.argtypes = [vp, C.POINTER(KerrConstants)]
     for name in EXPORTS:
         getattr(lib, name)   # every symbol of the header must resolve
     if path is None:
@@ -102,6 +116,12 @@ def default_params(problem_id: int) -> Params:
     p = Params()
     _check(None, load().pdeval_default_params(problem_id, C.byref(p)))
     return p
+
+
+def default_kerr_constants() -> KerrConstants:
+    k = KerrConstants()
+    _check(None, load().pdeval_default_kerr_constants(C.byref(k)))
+    return k
 
 
 def _check(ctx, rc: int):
@@ -117,7 +137,8 @@ def _ptr(a: Optional[np.ndarray]):
 class Context:
     """One libpdeval context = one GPU + one problem's sample grid."""
 
-    def __init__(self, problem_id: int, device: int = 0, grid: Optional[np.ndarray] = None):
+    def __init__(self, problem_id: int, device: int = 0, grid: Optional[np.ndarray] = None,
+                 kerr: Optional[KerrConstants] = None):
         lib = load()
         h = C.c_void_p()
         gp = None
@@ -134,6 +155,12 @@ class Context:
         self.device = device
         self.n_ref = lib.pdeval_n_ref_points(h)
         self.n_points = lib.pdeval_n_points(h)
+        if kerr is not None:
+            self.set_kerr_constants(kerr)
+
+    def set_kerr_constants(self, k: KerrConstants):
+        """The Kerr constants of this context (pdeval_set_kerr_constants)."""
+        _check(self.h, self.lib.pdeval_set_kerr_constants(self.h, C.byref(k)))
 
     def close(self):
         if self.h:

@@ -34,7 +34,7 @@ from . import problem_defs as P
 from .flatten import Unsupported
 from .opcodes import (CLS_ACCEPT, CLS_BAD_PROGRAM, CLS_NONFINITE_REF, CLS_REJECT_GRID,
                       CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC, CLS_UNSUPPORTED, CLS_ZERO_GRADIENT, FLAG_RATIONAL,
-                      PROBLEM_FORCE_FREE)
+                      HAS_IMM, IMM_PRM, PROBLEM_FORCE_FREE, PROBLEM_KERR, op_len)
 
 
 @dataclass
@@ -121,14 +121,84 @@ def symbolic_zero_gradient(pd, items, out) -> List[int]:
     return rows
 
 
+def _has_prm(words) -> bool:
+    i = 1
+    while i < len(words):
+        w = int(words[i])
+        if (w & 0xff) in HAS_IMM and w & IMM_PRM:
+            return True
+        i += op_len(w)
+    return False
+
+
+def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-10,
+                           n_grid: int = 4096) -> List[int]:
+    """Kerr with a constant whose point-stage value is 0 (a_value = 0): the reference's fast
+    point check substitutes the values into the SYMBOLIC lhs (kerr validator.py:163-192), after
+    differentiation, so a u that is singular or undefined at a = 0 can still pass -- its lhs
+    may not contain a at all (``x + a**(-2)``), or be 0 * (a finite value) (``a**2/x**(-3/2)``
+    at x < 0).  The device evaluates u itself at the point and sees a non-finite value.  The
+    candidates it rejected at the point stage for non-finiteness (rejected with max|lhs| below
+    the threshold) and whose program uses the constants are re-checked here with the
+    reference's own rule; where it passes, the grid stage (evaluated at the stand-ins of the
+    symbols) decides: a failing point, or no finite point at all (the device's rule), rejects.
+    Updates ``out`` in place; returns the changed rows."""
+    if pd.problem_id != PROBLEM_KERR or kerr is None or kerr.a_num != 0:
+        return []
+    st = np.asarray(out['status'])
+    rows = []
+    for i in np.flatnonzero((st == CLS_REJECT_POINT) & ~(np.asarray(out['q_ref']) >= abs_tol)):
+        if not _has_prm(ops[off[i]:off[i + 1]]):
+            continue
+        try:
+            u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
+            if not _kerr_fast_point_check(pd, kerr, u, abs_tol):
+                continue
+        except Exception:   # noqa: BLE001  (the device's reject stands)
+            continue
+        no_grid = int(out['n_nonfinite'][i]) >= n_grid
+        st[i] = CLS_REJECT_GRID if (out['n_bad'][i] > 0 or no_grid) else CLS_ACCEPT
+        if 'verdict' in out:
+            out['verdict'][i] = st[i] == CLS_ACCEPT
+        rows.append(i)
+    return rows
+
+
+def _kerr_fast_point_check(pd, kerr, u, abs_tol) -> bool:
+    """kerr validator.py:77-91 (lhs) and :163-192 (the 3-point check) in SymPy."""
+    r, x = pd.x, pd.y
+    M = sp.Rational(kerr.M_num, kerr.M_den) if kerr.op_M_fixed else pd.constants['M']
+    a = sp.Rational(kerr.a_num, kerr.a_den) if kerr.op_a_fixed else pd.constants['a']
+    G = 1 - (2 * M * r) / (r**2 + a**2 * x**2)
+    lhs = sp.diff(G / (1 - x**2) * sp.diff(u, r), r) + sp.diff(G / (r**2 - 2 * M * r + a**2) * sp.diff(u, x), x)
+    base = {pd.constants['M']: sp.Rational(kerr.M_num, kerr.M_den),
+            pd.constants['a']: sp.Rational(kerr.a_num, kerr.a_den)}
+    worst, n_ok = 0.0, 0
+    for px, py in ((sp.Rational(5, 2), sp.Rational(3, 5)), (sp.Rational(7, 3), sp.Rational(1, 3)),
+                   (sp.Integer(5), sp.Rational(-2, 5))):
+        try:
+            v = sp.N(lhs.subs({**base, r: px, x: py}), 40)
+            if v.is_real is False:
+                return False
+            fv = float(v)
+            if fv != fv:
+                return False
+            worst = max(worst, abs(fv))
+            n_ok += 1
+        except Exception:   # noqa: BLE001  (the reference skips the point)
+            continue
+    return n_ok > 0 and worst < abs_tol
+
+
 class BatchValidator:
     """One problem on one GPU.  Thread-safe (calls are serialized per context)."""
 
-    def __init__(self, problem: str = 'force_free', device: int = 0, params=None):
-        from ._lib import Context, default_params
+    def __init__(self, problem: str = 'force_free', device: int = 0, params=None, kerr=None):
+        from ._lib import Context, default_params, default_kerr_constants
         self.pd = P.get(problem)
         self.device = device
-        self.ctx = Context(self.pd.problem_id, device=device)
+        self.kerr = kerr if kerr is not None or self.pd.problem_id != PROBLEM_KERR else default_kerr_constants()
+        self.ctx = Context(self.pd.problem_id, device=device, kerr=kerr)
         self.params = params if params is not None else default_params(self.pd.problem_id)
         self._lock = threading.Lock()
 
@@ -152,6 +222,8 @@ class BatchValidator:
     def _verdicts(self, ops, off, notes, items) -> List[Verdict]:
         r = self.run(ops, off)
         symbolic_zero_gradient(self.pd, items, r)
+        kerr_exact_point_check(self.pd, self.kerr, items, r, ops, off, self.params.kerr_abs_tol,
+                               self.ctx.n_points - self.ctx.n_ref)
         out = []
         for i in range(len(off) - 1):
             hdr = int(ops[off[i]])
@@ -179,14 +251,15 @@ class BatchValidator:
         self.ctx.close()
 
 
-_VALIDATORS: Dict[Tuple[str, int], BatchValidator] = {}
+_VALIDATORS: Dict[tuple, BatchValidator] = {}
 _VLOCK = threading.Lock()
 
 
-def get_validator(problem: str, device: int = 0) -> BatchValidator:
-    """Process-wide BatchValidator per (problem, device): one libpdeval context per GPU."""
-    key = (P.get(problem).slug, device)
+def get_validator(problem: str, device: int = 0, kerr=None) -> BatchValidator:
+    """Process-wide BatchValidator per (problem, device, Kerr constants): one libpdeval context
+    per GPU and parameter set."""
+    key = (P.get(problem).slug, device, kerr.key() if kerr is not None else None)
     with _VLOCK:
         if key not in _VALIDATORS:
-            _VALIDATORS[key] = BatchValidator(problem, device)
+            _VALIDATORS[key] = BatchValidator(problem, device, kerr=kerr)
         return _VALIDATORS[key]

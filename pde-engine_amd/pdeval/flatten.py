@@ -15,7 +15,11 @@ We take the same tree and compile it for the kernel:
   held in VGPRs on the device -- as shallow as the tree allows;
 * constants are folded to IEEE doubles (rationals correctly rounded from the exact p/q); a
   constant that is not exactly a double (1/3, 1/10, E) also carries the low part of its
-  double-double value (opcode flag IMM_DD) for the point stage's double-double tier.
+  double-double value (opcode flag IMM_DD) for the point stage's double-double tier;
+* the problem's constants (Kerr ``M``, ``a``) stay symbolic: a leaf whose immediate is a
+  descriptor (opcode flag IMM_PRM), given its value per stage by the device -- the validator's
+  M_value / a_value in the point stage, stand-ins of the symbols in the constant test and the
+  grid stage, as the reference keeps them symbolic there (kerr validator.py:231-300).
 
 The output is a list of int32 words: a header (opcode 0, stack depth in bits 8-15, flags in
 bits 16-31), then the postfix body; opcodes with an immediate are followed by its two words.
@@ -29,8 +33,9 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import sympy as sp
 
-from .opcodes import (PDOP, HAS_IMM, IMM_DD, P_OPS, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD,
-                      FLAG_RATIONAL, FLAG_NONSMOOTH2D, FLAG_UNPROVABLE, op_len)
+from .opcodes import (PDOP, HAS_IMM, IMM_DD, IMM_PRM, P_OPS, MAX_STACK, FLAG_COMPLEX, FLAG_NOCOORD,
+                      FLAG_RATIONAL, FLAG_NONSMOOTH2D, FLAG_UNPROVABLE, PRM_INV_M, PRM_M2, PRM_NAME, PRM_NEG,
+                      op_len)
 
 
 class Unsupported(Exception):
@@ -38,7 +43,7 @@ class Unsupported(Exception):
 
 
 # --------------------------------------------------------------------------- IR
-# nodes: ('x',) ('y',) ('i',) ('c', value, exact, rational)
+# nodes: ('x',) ('y',) ('i',) ('c', value, exact, rational) ('m', k) (the problem's constant k)
 #        (op, child) for op in neg sqrt exp log abs;  ('pown', child, n);  ('pow', child, alpha)
 #        (op, a, b) for op in add sub mul div
 # A constant keeps its exact value (a Fraction; E and pi to 60 digits) beside the rounded
@@ -54,7 +59,7 @@ def _is_pvar(n) -> bool:
 
 
 def _is_leaf(n) -> bool:
-    return n[0] in ('x', 'y', 'c') or _is_pvar(n)
+    return n[0] in ('x', 'y', 'c', 'm') or _is_pvar(n)
 
 
 def _cfrac(ex: Optional[Fraction], rational: bool = True) -> tuple:
@@ -99,10 +104,10 @@ def _num_to_float(e: sp.Basic) -> float:
 
 
 class _Lower:
-    def __init__(self, x_sym: sp.Symbol, y_sym: sp.Symbol, consts: Dict[sp.Symbol, sp.Basic]):
+    def __init__(self, x_sym: sp.Symbol, y_sym: sp.Symbol, params: Dict[sp.Symbol, int]):
         self.x = x_sym
         self.y = y_sym
-        self.consts = consts
+        self.params = params
         self.uses_i = False
         self.irrational_const = False
 
@@ -112,9 +117,9 @@ class _Lower:
                 return ('x',)
             if e == self.y or e.name == self.y.name:
                 return ('y',)
-            for s, v in self.consts.items():
+            for s, k in self.params.items():
                 if e == s or e.name == s.name:
-                    return _cnum(sp.nsimplify(v) if not isinstance(v, float) else sp.Float(v))
+                    return ('m', k)
             raise Unsupported(f'free symbol {e}')
         if e is sp.nan or e is sp.zoo or e is sp.oo or e is sp.S.NegativeInfinity:
             return _cfrac(None)     # the driver's pre-validate filter drops these
@@ -217,6 +222,8 @@ class _Lower:
     def _pown(self, b, n: int):
         if n == 1:
             return b
+        if n == 2 and b[0] == 'm' and b[1] < 4:      # M**2, a**2: a constant of the problem too
+            return ('m', b[1] + PRM_M2)
         if n <= 16:
             return ('pown', b, n)
         return ('pow', b, float(n))
@@ -245,14 +252,14 @@ class _Lower:
 def _need(n) -> int:
     """Stack slots needed to evaluate node n (fused leaf operands need none)."""
     k = n[0]
-    if k in ('x', 'y', 'c', 'i'):
+    if k in ('x', 'y', 'c', 'i', 'm'):
         return 1
     if k in ('neg', 'sqrt', 'exp', 'log', 'abs', 'pown', 'pow'):
         return _need(n[1])
     a, b = n[1], n[2]
     if _is_leaf(b) and k in ('add', 'sub', 'mul', 'div'):
         return _need(a)
-    if _is_leaf(a) and k in ('add', 'mul', 'sub') or (k == 'div' and (a[0] == 'c' or _is_pvar(a))):
+    if _is_leaf(a) and k in ('add', 'mul', 'sub') or (k == 'div' and (a[0] in ('c', 'm') or _is_pvar(a))):
         return _need(b)
     na, nb = _need(a), _need(b)
     if na == nb:
@@ -265,6 +272,15 @@ class _Emit:
         self.w: List[int] = []
         self.d = 0
         self.dmax = 0
+
+    def op_prm(self, name: str, desc: int):
+        """An immediate opcode whose immediate is the problem's constant `desc` (PRM_*)."""
+        self.w.append(PDOP[name] | IMM_PRM)
+        self.w.append(desc)
+        self.w.append(0)
+        if name == 'PUSH_C':
+            self.d += 1
+            self.dmax = max(self.dmax, self.d)
 
     def op(self, name: str, imm: Optional[float] = None, arg: int = 0, imm_lo: float = 0.0):
         code = PDOP[name]
@@ -295,6 +311,8 @@ class _Emit:
             self.op('PUSH_Y')
         elif n[0] == 'i':
             self.op('PUSH_I')
+        elif n[0] == 'm':
+            self.op_prm('PUSH_C', n[1])
         else:
             self.op('PUSH_C', n[1], imm_lo=_clo(n))
 
@@ -304,6 +322,17 @@ class _Emit:
         if _is_pvar(leaf):
             self.op({'add': 'ADD_P', 'sub': 'SUB_P', 'mul': 'MUL_P', 'div': 'DIV_P'}[k],
                     arg=self._parg(leaf))
+            return True
+        if t == 'm':
+            p = leaf[1]
+            if k == 'add':
+                self.op_prm('ADDC', p)
+            elif k == 'sub':
+                self.op_prm('ADDC', p | PRM_NEG)
+            elif k == 'mul':
+                self.op_prm('MULC', p)
+            else:
+                self.op_prm('MULC', p ^ PRM_INV_M)     # / M = * (1/M)
             return True
         if t == 'c':
             c = leaf[1]
@@ -328,7 +357,7 @@ class _Emit:
 
     def emit(self, n):
         k = n[0]
-        if k in ('x', 'y', 'c', 'i') or _is_pvar(n):
+        if k in ('x', 'y', 'c', 'i', 'm') or _is_pvar(n):
             self.leaf(n)
             return
         if k in ('neg', 'sqrt', 'exp', 'log', 'abs'):
@@ -361,6 +390,10 @@ class _Emit:
             self.emit(b)
             self.op('RDIVC', a[1], imm_lo=_clo(a))
             return
+        if k == 'div' and a[0] == 'm':          # M / b
+            self.emit(b)
+            self.op_prm('RDIVC', a[1])
+            return
         if k == 'div' and _is_pvar(a):          # v**n / b
             self.emit(b)
             self.op('RDIV_P', arg=self._parg(a))
@@ -382,9 +415,10 @@ def _s32(u: int) -> int:
 
 # --------------------------------------------------------------------------- public API
 def lower(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
-          consts: Optional[Dict[sp.Symbol, sp.Basic]] = None):
-    """SymPy tree -> IR node (raises Unsupported).  Returns (ir, uses_i, rational_consts)."""
-    lw = _Lower(x_sym, y_sym, consts or {})
+          params: Optional[Dict[sp.Symbol, int]] = None):
+    """SymPy tree -> IR node (raises Unsupported).  Returns (ir, uses_i, rational_consts).
+    params: the problem's constants (symbol -> PRM_* index), kept symbolic."""
+    lw = _Lower(x_sym, y_sym, params or {})
     return lw.node(expr), lw.uses_i, not lw.irrational_const
 
 
@@ -431,7 +465,7 @@ def _det_kind(n):
     is prod h_k**(6 a_k) times a rational function: rational iff every 6 a_k is an integer.
     """
     k = n[0]
-    if k in ('x', 'y'):
+    if k in ('x', 'y', 'm'):     # (a constant of the problem: rational in the point stage)
         return 'R'
     if k == 'c':
         return 'R' if n[3] else 'C'
@@ -502,16 +536,16 @@ def det_rational(ir) -> bool:
             continue
         if k in ('add', 'sub'):
             a, b = n[1], n[2]
-            if a[0] == 'c' or _det_kind(a) == 'C':
+            if a[0] in ('c', 'm') or _det_kind(a) == 'C':
                 n = b
                 continue
-            if b[0] == 'c' or _det_kind(b) == 'C':
+            if b[0] in ('c', 'm') or _det_kind(b) == 'C':
                 n = a
                 continue
-        elif k == 'mul' and n[1][0] == 'c' and n[1][3]:
+        elif k == 'mul' and (n[1][0] == 'm' or n[1][0] == 'c' and n[1][3]):
             n = n[2]
             continue
-        elif k in ('mul', 'div') and n[2][0] == 'c' and n[2][3]:
+        elif k in ('mul', 'div') and (n[2][0] == 'm' or n[2][0] == 'c' and n[2][3]):
             n = n[1]
             continue
         break
@@ -544,9 +578,9 @@ def compile_ir(ir, uses_i: bool = False, rational_consts: bool = True) -> List[i
 
 
 def flatten(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
-            consts: Optional[Dict[sp.Symbol, sp.Basic]] = None) -> List[int]:
+            params: Optional[Dict[sp.Symbol, int]] = None) -> List[int]:
     """SymPy expression -> program words (header first).  Raises Unsupported."""
-    ir, uses_i, rational_consts = lower(expr, x_sym, y_sym, consts)
+    ir, uses_i, rational_consts = lower(expr, x_sym, y_sym, params)
     words = compile_ir(ir, uses_i, rational_consts)
     if unprovable(expr):
         words[0] |= FLAG_UNPROVABLE
@@ -573,7 +607,12 @@ def disasm(words: Sequence[int]) -> str:
         w = int(words[i]) & 0xffffffff
         op = w & 0xff
         name = OP_NAME.get(op, f'?{op}')
-        if op in HAS_IMM:
+        if op in HAS_IMM and w & IMM_PRM:
+            dsc = int(words[i + 1])
+            v = ('-' if dsc & PRM_NEG else '') + PRM_NAME[dsc & 7]
+            out.append(f'{name} {v}')
+            i += op_len(w)
+        elif op in HAS_IMM:
             lo, hi = int(words[i + 1]) & 0xffffffff, int(words[i + 2]) & 0xffffffff
             v = struct.unpack('<d', struct.pack('<II', lo, hi))[0]
             if w & IMM_DD:

@@ -17,6 +17,12 @@ OP_NAME = {v: k for k, v in PDOP.items()}
 HAS_IMM = {PDOP['PUSH_C'], PDOP['ADDC'], PDOP['MULC'], PDOP['RDIVC'], PDOP['POW']}
 # bit 8 of an immediate-carrying opcode word: a double-double low part (2 more words) follows
 IMM_DD = 1 << 8
+# bit 9: the immediate is one of the problem's constants (Kerr M, a): descriptor word, then 0
+IMM_PRM = 1 << 9
+# descriptor: bits 0-2 {M, a, 1/M, 1/a, M^2, a^2, 1/M^2, 1/a^2} (index ^ 2: the reciprocal,
+# index + 4: the square), bit 3: negated
+PRM_M, PRM_A, PRM_INV_M, PRM_INV_A, PRM_M2, PRM_A2, PRM_NEG = 0, 1, 2, 3, 4, 5, 8
+PRM_NAME = {0: 'M', 1: 'a', 2: '1/M', 3: '1/a', 4: 'M**2', 5: 'a**2', 6: '1/M**2', 7: '1/a**2'}
 
 
 def op_len(word: int) -> int:

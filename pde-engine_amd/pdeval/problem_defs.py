@@ -2,9 +2,10 @@
 
 Mirrors the plugin registry of the reference (``problems/__init__.py:66-108`` force-free,
 ``:259-302`` Kerr) for what the validator needs: the two coordinates, the constants (Kerr
-``M = 1``, ``a = 1/10``, the values ``KerrMagnetosphereValidator`` substitutes,
-``kerr validator.py:36-37`` and ``problems/__init__.py:283``) and the locals mapping the driver
-hands to ``sympify`` (symbols + constants + UNARY_OPS, ``general_method_paper_reproduction.py:
+``M`` and ``a``, which programs keep symbolic: the device gives them the validator's
+``M_value`` / ``a_value`` in the point stage, ``kerr validator.py:36-37, :163-171``, and
+stand-ins of the symbols in the constant test and the grid stage, ``:231-300``) and the locals
+mapping the driver hands to ``sympify`` (symbols + constants + UNARY_OPS, ``general_method_paper_reproduction.py:
 84-93``).
 """
 from __future__ import annotations
@@ -18,7 +19,7 @@ import numpy as np
 import sympy as sp
 
 from .flatten import Unsupported, flatten, pack
-from .opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR, PDOP
+from .opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR, PDOP, PRM_A, PRM_M
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if _PKG_ROOT not in sys.path:
@@ -33,7 +34,7 @@ class ProblemDef:
     x: sp.Symbol
     y: sp.Symbol
     constants: Dict[str, sp.Symbol]
-    const_values: Dict[sp.Symbol, sp.Basic]
+    params: Dict[sp.Symbol, int]          # the constants as program parameters (PRM_*)
     known_solutions: Dict[str, str] = field(default_factory=dict)
 
     @property
@@ -52,7 +53,7 @@ class ProblemDef:
         return sp.sympify(s, locals=self.sympify_locals)
 
     def compile(self, expr: sp.Basic) -> List[int]:
-        return flatten(expr, self.x, self.y, self.const_values)
+        return flatten(expr, self.x, self.y, self.params)
 
 
 def force_free() -> ProblemDef:
@@ -76,7 +77,7 @@ def kerr() -> ProblemDef:
     M = sp.Symbol('M', real=True, positive=True)
     a = sp.Symbol('a', real=True)
     return ProblemDef('kerr_magnetosphere', PROBLEM_KERR, r, x, {'M': M, 'a': a},
-                      {M: sp.Integer(1), a: sp.Rational(1, 10)},
+                      {M: PRM_M, a: PRM_A},
                       {'1 - x': 'Monopole (a -> 0 limit)'})   # problems/__init__.py:285-287
 
 

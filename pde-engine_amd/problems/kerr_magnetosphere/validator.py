@@ -7,6 +7,13 @@ defer_heavy_checks=True, enforce_anchor=None) -> (bool, str)`` (``:210-345``), `
 ``d_r[G/(1-x^2) d_r u] + d_x[G/Delta d_x u]`` (``:77-91``), the 3-point check (absolute 1e-10,
 ``:163-192``) and the exact-zero stage (``:283-315``) run on the GPU for whole batches.
 
+Any ``M_value`` / ``a_value`` (``:36-37``): the device's point stage substitutes them, as the
+reference's fast point check does, while its constant test and grid stage -- the surrogates of
+the reference's ``simplify(u)`` test and symbolic stage, which keep ``M`` and ``a`` symbolic --
+use stand-ins of the symbols (``pdeval_kerr_constants``, include/pdeval.h).  A validator built
+with a number for ``M`` or ``a`` (e.g. ``a = 0``, the Schwarzschild operator) uses that number
+in its operator everywhere; ``u``'s own symbol is then free.
+
 With ``defer_heavy_checks=False`` the reference's heavy checks on exact zeros (constancy,
 finiteness, axis/horizon regularity, a -> 0 monopole anchor, ``:325-342``) run on the host in
 SymPy -- only for the (rare) candidates the GPU accepts.
@@ -25,8 +32,7 @@ class KerrMagnetosphereValidator:
                  require_monopole_extension: bool = True, monopole_target: str = '1-x',
                  allow_normalization: bool = False, strict_sympy_check: bool = True,
                  exclude_constants: bool = True, device: int = 0) -> None:
-        if sp.nsimplify(M_value) != 1 or sp.nsimplify(a_value) != sp.Rational(1, 10):
-            raise NotImplementedError('the device operator tables are built for M = 1, a = 1/10')
+        self._kerr = self.device_constants(M, a, M_value, a_value)
         self.r, self.x, self.M, self.a = r, x, M, a
         self.M_value, self.a_value = M_value, a_value
         self.use_lean = use_lean
@@ -41,10 +47,28 @@ class KerrMagnetosphereValidator:
         self._last_evidence: Dict[str, Any] = {}
         self._bv = None
 
+    @staticmethod
+    def device_constants(M, a, M_value, a_value):
+        """pdeval_kerr_constants for this validator: exact rationals M_value, a_value; the
+        operator's M (a) fixed when the constructor got a number for it (which must then be
+        the value the fast point check substitutes for it, ``:165-166``)."""
+        from pdeval._lib import default_kerr_constants
+        k = default_kerr_constants()
+        Mv, av = sp.Rational(sp.nsimplify(M_value)), sp.Rational(sp.nsimplify(a_value))
+        if not (Mv > 0 and abs(av) < Mv):
+            raise ValueError('Kerr constants: need M_value > 0 and |a_value| < M_value (a horizon)')
+        k.M_num, k.M_den, k.a_num, k.a_den = int(Mv.p), int(Mv.q), int(av.p), int(av.q)
+        for name, sym, val in (('M', M, Mv), ('a', a, av)):
+            if not isinstance(sym, sp.Symbol):
+                if sp.nsimplify(sym) != val:
+                    raise NotImplementedError(f'operator {name} = {sym} differs from {name}_value = {val}')
+                setattr(k, f'op_{name}_fixed', 1)
+        return k
+
     def _validator(self):
         if self._bv is None:
             from pdeval.batch import get_validator
-            self._bv = get_validator('kerr', self.device)
+            self._bv = get_validator('kerr', self.device, kerr=self._kerr)
         return self._bv
 
     # --------------------------------------------------------------- operator (host, symbolic)

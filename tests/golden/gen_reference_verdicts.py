@@ -44,7 +44,7 @@ def _alarm(_sig, _frm):
     raise _Timeout()
 
 
-def _init_worker(ref, problem):
+def _init_worker(ref, problem, kerr_a_value='1/10', kerr_op_a_zero=False):
     global _D
     os.chdir(ref)
     sys.path.insert(0, ref)
@@ -60,8 +60,12 @@ def _init_worker(ref, problem):
     else:
         from problems.kerr_magnetosphere.validator import KerrMagnetosphereValidator
         s, c = d.problem.symbols, d.problem.constants
-        v = KerrMagnetosphereValidator(s['r'], s['x'], c['M'], c['a'],
-                                       M_value=sp.Integer(1), a_value=sp.Rational(1, 10),
+        # the problem's validator (problems/__init__.py:283): M_value = 1, a_value = 1/10; a
+        # fixture run may pass another a_value (kerr validator.py:36-37), or build the operator
+        # with the number 0 for a (the Schwarzschild operator; u's a is then a free symbol)
+        a_op = sp.Integer(0) if kerr_op_a_zero else c['a']
+        v = KerrMagnetosphereValidator(s['r'], s['x'], c['M'], a_op,
+                                       M_value=sp.Integer(1), a_value=sp.Rational(kerr_a_value),
                                        use_lean=False)
         v.use_lean = True
         v._lean = LeanNormalizer(cache_db=':memory:')
@@ -162,6 +166,9 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--timeout', type=int, default=60)
     ap.add_argument('--procs', type=int, default=os.cpu_count())
+    ap.add_argument('--kerr-a-value', default='1/10', help="Kerr validator's a_value")
+    ap.add_argument('--kerr-op-a-zero', action='store_true',
+                    help='Kerr operator built with a = 0 (validator a argument = the number 0)')
     a = ap.parse_args()
     _TIMEOUT = a.timeout
     make_scratch_copy('/root/reference', a.ref)
@@ -207,11 +214,14 @@ def main():
         items = [it for it in items if it[1] == a.depth]
     if a.sample and a.sample < len(items):
         items = sorted(random.Random(a.seed).sample(items, a.sample))
-    with mp.get_context('fork').Pool(a.procs, _init_worker, (a.ref, a.problem),
+    init = (a.ref, a.problem, a.kerr_a_value, a.kerr_op_a_zero)
+    with mp.get_context('fork').Pool(a.procs, _init_worker, init,
                                      maxtasksperchild=200) as pool, open(a.out, 'w') as f:
         n = 0
         for rec in pool.imap_unordered(_verdict_one, items, chunksize=1):
             rec['problem'] = a.problem
+            if a.problem != 'force_free' and (a.kerr_a_value != '1/10' or a.kerr_op_a_zero):
+                rec['kerr'] = {'M_value': '1', 'a_value': a.kerr_a_value, 'op_a_zero': a.kerr_op_a_zero}
             f.write(json.dumps(rec) + '\n')
             f.flush()
             n += 1

@@ -29,13 +29,28 @@ FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl', 
           'ff_d4_exp_quarter.jsonl', 'ff_d4_t600.jsonl')
 KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl', 'kerr_d4_s2000.jsonl',
             'kerr_d4_accepts.jsonl')
-# Kerr candidates whose reason class differs from the reference's, with the same verdict: the
-# device and the oracle substitute M = 1, a = 1/10 before validating (the reference's point
-# check values), while the reference's constant test and symbolic stage keep M and a symbolic
-# (kerr validator.py:231-240, :279-300).  This u is constant only at M = 1: here "Trivial
-# constant solution excluded", there "PDE residual != 0".  (1 of the 1,024,799
-# candidates of the Kerr depth<=4 stream.)
-KERR_PARAM_CLASS = {'exp(a**2)*exp(2*r)*exp(-2*M*r)'}
+# The reference's Kerr validator at other constants (gen_reference_verdicts.py --kerr-a-value 0
+# [--kerr-op-a-zero]): a_value = 0 with M and a symbolic (kerr validator.py:36-44: the fast point
+# check substitutes a = 0, the constant test and the symbolic stage keep a symbolic, so u = 1 - x
+# passes the point check and fails the symbolic stage), and the operator built with the number
+# 0 for a (the Schwarzschild operator; u's own a is then a free symbol): the reference accepts
+# 66 of these (61 of the streams, 5 edge cases), the only Kerr accepts it produces (forms
+# c1 + c2*x, with c1, c2 free of r and x).  The edge files (edge_kerr2.txt) hold the rules'
+# corner cases: stationary at the reference points, constant only at M = 1, underflow on the
+# grid, not real on the grid, u == 0, singular at a = 0, a pole at a reference point.
+KERR_A0 = ('kerr_a0_d1.jsonl', 'kerr_a0_d2.jsonl', 'kerr_a0_d3_s1000.jsonl', 'kerr_a0_edge.jsonl')
+KERR_OP0 = ('kerr_op0_d1.jsonl', 'kerr_op0_d2.jsonl', 'kerr_op0_d3_s1000.jsonl', 'kerr_op0_edge.jsonl')
+# One reason-class divergence, same verdict (False): with the Schwarzschild operator u's own a
+# is a free symbol, so the reference cannot evaluate an lhs that contains it and rejects at its
+# fast point check ("Indeterminate", kerr validator.py:186-189); the device evaluates u's a at
+# its stand-in, where this u underflows to 0 at every reference point, and rejects at the grid.
+KERR_CLASS_DIVERGENCE = {('operator_a=0', 'exp_neg(E*exp(r**2)*exp(a**2*x**2))')}
+# configuration -> (pdeval_kerr_constants fields, fixture files)
+KERR_CONFIGS = {
+    'a=1/10': ((1, 1, 1, 10, 1.171875, 0.359375, 0, 0), KERR_REF + ('kerr_edge.jsonl', 'kerr_edge2.jsonl')),
+    'a_value=0': ((1, 1, 0, 1, 1.171875, 0.359375, 0, 0), KERR_A0),
+    'operator_a=0': ((1, 1, 0, 1, 1.171875, 0.359375, 0, 1), KERR_OP0),
+}
 # Force-free candidates whose reject TEXT differs, with the same verdict and the same stage:
 # when the reference's symbolic stage is reached with a determinant whose string is >= 3000
 # characters it expands instead of calling Lean and prints "Invalid (expanded det != 0)"
@@ -48,3 +63,57 @@ def exact_rows(name='ff_d4_exact_det.jsonl'):
     """Exact-arithmetic ground truth (gen_exact_det.py): det_zero = true solution."""
     with open(os.path.join(GOLDEN, 'exact', name)) as f:
         return [json.loads(l) for l in f]
+
+
+# Force-free fixture candidates whose grid counts differ between the device and the oracle,
+# with the class equal: (|n_bad difference|, |n_nonfinite difference|), measured by
+# scripts/tolerance_survey.py on the MI355X (profiles/r03_tolerance_survey.log).  n_bad differs
+# only on point rejects, where it is a reported tier-1 count whose points with q near tau_grid
+# depend on the evaluation order (device Horner vs oracle explicit powers); n_nonfinite only on
+# exp(exp(..)) candidates whose jets overflow near the 2^160 guard at a few grid points.  Every
+# other candidate's counts are equal exactly (tests/test_gpu_parity.py).
+FF_COUNT_SLACK = {
+    '1/(-rho/(-rho + z**2 + z) + 1)': (8, 0),
+    '1/(-rho/(-rho**2*z + z**3 + z) + z)': (7, 0),
+    '1/(-rho/(-rho**2*z + z**3 + z**2) + 1)': (11, 0),
+    '1/(-rho/(-rho**2*z**2 + z**4 + z**2) + 1)': (9, 0),
+    '1/(1 - 1/(-rho**2 + z**3 + 1))': (6, 0),
+    '1/(rho/(-rho**2*z + z**3 + z) - z)': (7, 0),
+    'exp(rho/(1 - 1/(-rho**2 + z**2 + 1)))': (6, 0),
+    'exp(z/(1 - 1/(-rho**2 + z**2 + 1)))': (6, 0),
+    'exp_neg(exp(rho**2)*exp(z**2/(-rho/z + 1)))': (0, 8),
+    'exp_neg(exp(rho**2)*exp(z**2/(1 - rho)))': (0, 20),
+    'exp_neg(exp(rho/(-rho*z + z)))': (0, 16),
+    'exp_neg(exp(rho/(-rho/z + 1)))': (0, 4),
+    'exp_neg(exp(z/(-rho/z + 1)))': (0, 4),
+    'exp_neg(exp(z/(1 - rho)))': (0, 2),
+    'inv(-rho/(-rho**2*z + z**3 + z) + z)': (7, 0),
+    'inv(rho/(-rho**2*z + z**3 + z) - z)': (7, 0),
+    'pow_neg_3_2(exp(rho/(-rho/z + 1)))': (0, 4),
+    'pow_neg_3_2(exp(z/(-rho/z + 1)))': (0, 4),
+    'pow_neg_3_2(exp_neg(rho/(-rho/z + 1)))': (0, 4),
+    'pow_neg_3_2(exp_neg(z/(-rho/z + 1)))': (0, 4),
+    'rho**2 + z**2/(-rho/(-rho + z**2 + z) + 1)': (1, 0),
+    'rho**2 + z**2/(-rho/(-rho**2*z + z**3 + z) + z)': (2, 0),
+    'rho**2 + z**2/(-rho/(-rho**2*z**2 + z**4 + z**2) + 1)': (5, 0),
+    'rho**2 + z**2/(1 - 1/(-rho**2 + z**3 + 1))': (2, 0),
+    'rho**2 + z**2/(rho/(-rho**2*z + z**3 + z) - z)': (5, 0),
+    'rho/(-rho*z/(-rho + z**2 + z) + z)': (12, 0),
+    'rho/(-rho*z/(-rho**2*z + z**3 + z) + z**2)': (7, 0),
+    'rho/(-rho*z/(-rho**2*z + z**3 + z**2) + z)': (12, 0),
+    'rho/(-rho/(-rho + z**2 + z) + 1)': (7, 0),
+    'rho/(-rho/(-rho**2*z + z**3 + z) + z)': (9, 0),
+    'rho/(-rho/(-rho**2*z + z**3 + z**2) + 1)': (7, 0),
+    'rho/(-rho/(-rho**2*z**2 + z**4 + z**2) + 1)': (7, 0),
+    'rho/(1 - 1/(-rho**2 + z**3 + 1))': (2, 0),
+    'rho/(rho*z/(-rho**2*z + z**3 + z) - z**2)': (7, 0),
+    'rho/(rho/(-rho**2*z + z**3 + z) - z)': (9, 0),
+    'rho/(z*(1 - 1/(-rho**2 + z**3 + 1)))': (4, 0),
+    'z/(-rho/(-rho + z**2 + z) + 1)': (10, 0),
+    'z/(-rho/(-rho**2*z + z**3 + z) + z)': (7, 0),
+    'z/(-rho/(-rho**2*z + z**3 + z**2) + 1)': (5, 0),
+    'z/(-rho/(-rho**2*z**2 + z**4 + z**2) + 1)': (7, 0),
+    'z/(1 - 1/(-rho**2 + z**3 + 1))': (4, 0),
+    'z/(rho*(1/(-rho**2*z + z**3 + z) - 1/z) + 1 - 1/(-rho**2 + z**2 + 1))': (7, 0),
+    'z/(rho/(-rho**2*z + z**3 + z) - z)': (7, 0),
+}

@@ -16,8 +16,9 @@ extern "C" int sim_point(int problem, const int32_t* w, int nw, double x, double
         std::vector<double> stk((MAXD - 1) * 15 * 64), es((MAXD - 1) * 15 * 64);
         I::J u;
         double e[15] = {0};
-        int rc = tier2 ? E::run(w, 1, nw, x, y, u, e, stk.data(), es.data(), 0)
-                       : I::run(w, 1, nw, x, y, u, stk.data(), 0);
+        const PrmTab<double> P{};   // (force-free: no constants of the problem)
+        int rc = tier2 ? E::run(w, 1, nw, x, y, u, e, stk.data(), es.data(), 0, P)
+                       : I::run(w, 1, nw, x, y, u, stk.data(), 0, P);
         if (rc) return rc;
         for (int i = 0; i < 15; ++i) { jet[i] = u.c[i]; err[i] = e[i]; }
         PointResult r = ff_epilogue<double>(u.c, x);
@@ -73,6 +74,10 @@ extern "C" int sim_point_tier(int problem, const int32_t* w, int nw, int k, int 
             for (int j = 0; j < 4; ++j) kc[4 * i + j] = a.kc_ref[4 * i + j].hi;
         }
         a.kc = kc;
+        // the point stage's constants: M_value = 1, a_value = 1/10 (PDEVAL_IMM_PRM)
+        a.prm_pt = PrmTab<double>{{1.0, 0.1, 1.0, 10.0, 1.0, 0.01, 1.0, 100.0}};
+        a.prm_pt_dd = PrmTab<dd>{{dd_from(1.0), dd_ratio(1.0, 10.0), dd_from(1.0), dd_from(10.0), dd_from(1.0),
+                                  dd_ratio(1.0, 100.0), dd_from(1.0), dd_from(100.0)}};
     }
     for (int i = 0; i < a.n_ref; ++i) {
         a.ref_x[i] = a.ref_xd[i].hi;

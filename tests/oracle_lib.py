@@ -24,7 +24,20 @@ def load():
                                          vp, C.c_int64, C.c_int64]
         _lib.oracle_jet.argtypes = [C.c_int, vp, C.c_int64, C.c_double, C.c_double, C.c_int, vp, vp]
         _lib.oracle_point.argtypes = [C.c_int, vp, C.c_int64, C.c_double, C.c_double, C.c_int, vp]
+        _lib.oracle_set_kerr_constants.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int64,
+                                                   C.c_double, C.c_double, C.c_int, C.c_int]
     return _lib
+
+
+DEFAULT_KERR = (1, 1, 1, 10, 1.171875, 0.359375, 0, 0)   # pdeval_default_kerr_constants
+
+
+def set_kerr_constants(k=DEFAULT_KERR):
+    """The oracle's Kerr constants (a pdeval._lib.KerrConstants or the 8-tuple of its fields);
+    process-wide: set it before validating, not while another thread validates."""
+    if hasattr(k, 'key'):
+        k = k.key()
+    load().oracle_set_kerr_constants(*k)
 
 
 class _Params(C.Structure):
@@ -102,7 +115,7 @@ def validate_mt(problem_id, ops, offsets, prm=None, threads=None, chunk=64):
     def run(first):
         lib.oracle_validate(problem_id, ops.ctypes.data, offsets.ctypes.data, n, C.addressof(prm),
                             *ptrs, first, min(chunk, n - first))
-    threads = threads or min(16, int(os.environ.get('OMP_NUM_THREADS', '0') or os.cpu_count() or 1))
+    threads = threads or max(1, min(16, int(os.environ.get('OMP_NUM_THREADS') or 0) or os.cpu_count() or 1))
     with ThreadPoolExecutor(threads) as ex:
         list(ex.map(run, range(0, n, chunk)))
     out['res_ref'] = out['res_ref'].reshape(n, nref)

@@ -51,25 +51,21 @@ def _cmp_device_oracle(ctx, pd_, strings):
     ora = O.validate(pd_.problem_id, ops, off)
     assert np.array_equal(dev['status'], ora['status']), \
         [(s, int(a), int(b)) for s, a, b in zip(strings, dev['status'], ora['status']) if a != b][:10]
-    # n_bad decides the grid stage (tier 2 counts for grid rejects): equal wherever the grid
-    # decides; for a point reject (full_grid) it is only reported, a tier-1 count whose points
-    # near tau_grid depend on the evaluation order (device Horner vs oracle powers): 1 %.  A
-    # constant u (ZERO_GRADIENT, decided before the grid count) has a pure-noise residual: the
-    # device reports its tier-1 count without re-deciding it in tier 2, the oracle its tier-2
-    # count -- only reported, not compared
+    # grid counts: equal for every candidate, exactly, except
+    #  * a constant u (ZERO_GRADIENT, decided before the grid): its residual is rounding noise
+    #    (or exactly 0, by evaluation order), its counts are reported only;
+    #  * the force-free candidates listed in golden_data.FF_COUNT_SLACK (measured): tier-1
+    #    counts of point rejects near tau_grid, and jets overflowing near the 2^160 guard --
+    #    within the listed per-candidate amounts
     st = dev['status']
-    bad = np.flatnonzero((dev['n_bad'] != ora['n_bad']) & (st != 1) & (st != 3))
-    assert not bad.size, [(strings[i], int(dev['status'][i]), int(dev['n_bad'][i]), int(ora['n_bad'][i]))
-                          for i in bad[:10]]
-    nb = np.abs(dev['n_bad'].astype(np.int64) - ora['n_bad']) * (st != 3)
-    assert nb.max(initial=0) <= 41, [(strings[i], int(dev['n_bad'][i]), int(ora['n_bad'][i]))
-                                     for i in np.flatnonzero(nb > 41)[:10]]
-    # n_nonfinite: points where an intermediate jet of the program overflows (exp(exp(..)))
-    # depend on the evaluation order (device Horner vs oracle explicit powers); allow 1 % of
-    # the grid there -- the classes above are exact
-    d = np.abs(dev['n_nonfinite'].astype(np.int64) - ora['n_nonfinite'])
-    assert d.max(initial=0) <= 41, [(strings[i], int(dev['n_nonfinite'][i]), int(ora['n_nonfinite'][i]))
-                                    for i in np.flatnonzero(d > 41)[:10]]
+    bad = []
+    for i in np.flatnonzero(((dev['n_bad'] != ora['n_bad']) | (dev['n_nonfinite'] != ora['n_nonfinite'])) & (st != 3)):
+        nb, nf = G.FF_COUNT_SLACK.get(strings[i], (0, 0)) if pd_.problem_id == 0 else (0, 0)
+        if abs(int(dev['n_bad'][i]) - int(ora['n_bad'][i])) > nb or \
+                abs(int(dev['n_nonfinite'][i]) - int(ora['n_nonfinite'][i])) > nf:
+            bad.append((strings[i], int(st[i]), int(dev['n_bad'][i]), int(ora['n_bad'][i]),
+                        int(dev['n_nonfinite'][i]), int(ora['n_nonfinite'][i])))
+    assert not bad, bad[:10]
     check_residuals(dev, ora, strings)
     return dev, ora
 
@@ -149,8 +145,7 @@ def test_plugin_api_reasons_kerr():
     got = prob.validator.validate_batch(us, check_regularity=False, fast_point_only=False,
                                         lean_first=True, defer_heavy_checks=True, enforce_anchor=False)
     bad = [(r['expr'], r['reason'][:60], g[1][:60]) for g, r in zip(got, rows)
-           if g[0] != r['ok'] or (g[1].split('|')[0] != r['reason'].split('|')[0] and
-                                  r['expr'] not in G.KERR_PARAM_CLASS)]
+           if g[0] != r['ok'] or g[1].split('|')[0] != r['reason'].split('|')[0]]
     assert not bad, bad[:10]
     assert prob.validator.validate(us[0], check_regularity=False) == got[0]
 
@@ -401,3 +396,54 @@ def test_sharded_chain_world1_native_and_torch_gather():
     finally:
         dist.destroy_process_group()
         ctx.close()
+
+
+@pytest.mark.parametrize('cfg', list(G.KERR_CONFIGS))
+def test_kerr_constants_configs(cfg):
+    """Kerr at other constants (pdeval_set_kerr_constants): the reference's validator at
+    a = 1/10, at a_value = 0 (point check at a = 0, constant test and symbolic stage symbolic in
+    a, kerr validator.py:163-192, :231-300) and with the Schwarzschild operator (a = 0 in the
+    operator; 66 reference accepts).  Device class == oracle class for every fixture; the
+    plugin object, built as the reference's was, answers with the reference's verdict and
+    reason class for every decided fixture."""
+    import sympy as sp
+    from pdeval import _lib
+    from pdeval.batch import kerr_exact_point_check
+    from problems import load_problem
+    kc, files = G.KERR_CONFIGS[cfg]
+    pd_ = P.kerr()
+    rows = G.decided(G.ref_rows(*files))
+    strings = [r['expr'] for r in rows]
+    ops, off, _ = P.compile_strings(pd_, strings)
+    ctx = Context(1, kerr=_lib.KerrConstants(*kc))
+    dev = ctx.validate(ops, off)
+    O.set_kerr_constants(kc)
+    try:
+        ora = O.validate_mt(1, ops, off)
+    finally:
+        O.set_kerr_constants()
+    diff = np.flatnonzero(dev['status'] != ora['status'])
+    assert not diff.size, [(strings[i], int(dev['status'][i]), int(ora['status'][i])) for i in diff[:10]]
+    fixed = kerr_exact_point_check(pd_, _lib.KerrConstants(*kc), strings, dev, ops, off)
+    ref = np.array([bool(r['ok']) for r in rows])
+    assert np.array_equal(dev['verdict'], ref), [(strings[i], rows[i]['reason'][:50]) for i in
+                                                 np.flatnonzero(dev['verdict'] != ref)[:10]]
+    ctx.close()
+    # the drop-in plugin, constructed like the reference's (problems/__init__.py:283)
+    from problems.kerr_magnetosphere.validator import KerrMagnetosphereValidator
+    prob = load_problem('kerr_magnetosphere')
+    s, c = prob.symbols, prob.constants
+    a_op = sp.Integer(0) if kc[-1] else c['a']
+    v = KerrMagnetosphereValidator(s['r'], s['x'], c['M'], a_op, M_value=sp.Integer(1),
+                                   a_value=sp.Rational(kc[2], kc[3]))
+    locs = {**s, **c, **prob.unary_ops}
+    got = v.validate_batch([sp.sympify(t, locals=locs) for t in strings], check_regularity=False,
+                           fast_point_only=False, lean_first=True, defer_heavy_checks=True,
+                           enforce_anchor=False)
+    bad = [(r['expr'], r['reason'][:60], g[1][:60]) for g, r in zip(got, rows)
+           if g[0] != r['ok'] or (g[1].split('|')[0] != r['reason'].split('|')[0] and
+                                  (cfg, r['expr']) not in G.KERR_CLASS_DIVERGENCE)]
+    assert not bad, bad[:10]
+    if kc[-1]:
+        assert sum(g[0] for g in got) == 66
+    assert cfg != 'a_value=0' or len(fixed) >= 3     # the host step took part
