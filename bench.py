@@ -307,26 +307,57 @@ def main():
         dist.destroy_process_group()
 
 
-def worker_throughput(exprs, batch=4096):
-    """process_batch (pdeval/worker.py) over every validated d4 string in queue-sized batches:
-    native compile, one device call, known-solution tags; candidates/s end to end."""
+def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
+    """The drop-in paths over every validated d4 string (the reference's worker protocol,
+    general_method_paper_reproduction.py:1756-1816, queue tuples in -> result tuples out):
+    * process_batch, one queue-sized batch at a time (native compile, one device call,
+      vectorized reasons, known-solution tags);
+    * process_batches, the worker loop's pipeline (batch k+1 compiles on host threads while
+      batch k is on the device), at the default queue batch and at a larger one -- its result
+      tuples must equal process_batch's;
+    * the inline path: one validate(sympify(s)) per candidate, as the driver's sequential loop
+      calls it (:1299-1316), on a seeded sample."""
+    import random
+    import sympy as sp
     from problems import load_problem
-    from pdeval.worker import KnownSolutionTagger, filtered_kwargs, process_batch
+    from pdeval.native import host_threads
+    from pdeval.worker import KnownSolutionTagger, filtered_kwargs, process_batch, process_batches
     prob = load_problem('force_free')
     locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
     tagger = KnownSolutionTagger(prob, locs)
     kw = filtered_kwargs(prob.validator)
     items = [(i + 1, str(s)) for i, s in enumerate(exprs)]
     process_batch(items[:batch], prob.validator, kw, locs, tagger)      # warm
+    out = {'candidates': len(items), 'host_threads': host_threads()}
     t0 = time.perf_counter()
-    n_valid = n_tag = 0
+    ref = []
     for k in range(0, len(items), batch):
-        out = process_batch(items[k:k + batch], prob.validator, kw, locs, tagger)
-        n_valid += sum(1 for t in out if t[1])
-        n_tag += sum(1 for t in out if t[3])
+        ref.extend(process_batch(items[k:k + batch], prob.validator, kw, locs, tagger))
     dt = time.perf_counter() - t0
-    return {'candidates': len(items), 'batch': batch, 'seconds': round(dt, 3),
-            'candidates_per_s': round(len(items) / dt), 'valid': n_valid, 'paper_tagged': n_tag}
+    out['process_batch'] = {'batch': batch, 'seconds': round(dt, 3), 'candidates_per_s': round(len(items) / dt),
+                            'valid': sum(1 for t in ref if t[1]), 'paper_tagged': sum(1 for t in ref if t[3])}
+    for b in (batch, pipe_batch):
+        t0 = time.perf_counter()
+        got = []
+        for r in process_batches((items[k:k + b] for k in range(0, len(items), b)), prob.validator, kw, locs,
+                                 tagger):
+            got.extend(r)
+        dt = time.perf_counter() - t0
+        out[f'pipelined_b{b}'] = {'seconds': round(dt, 3), 'candidates_per_s': round(len(items) / dt),
+                                  'tuples_identical': got == ref}
+    sample = random.Random(0).sample(items, min(inline_n, len(items)))
+    v = prob.validator
+    t0 = time.perf_counter()
+    n_ok = 0
+    for _, s in sample:
+        ok, _ = v.validate(sp.sympify(s, locals=locs), **kw)
+        n_ok += bool(ok)
+    dt = time.perf_counter() - t0
+    out['inline_validate'] = {'sample': len(sample), 'seconds': round(dt, 3),
+                              'candidates_per_s': round(len(sample) / dt), 'valid': n_ok}
+    best = max(out[k]['candidates_per_s'] for k in out if k.startswith('pipelined'))
+    out['candidates_per_s'] = best
+    return out
 
 
 def cpu_baseline_sympy(procs, budget_s):

@@ -308,6 +308,22 @@ const char* pdeval_version(void);
 int pdeval_compile_batch(int problem_id, const char* text, const int64_t* str_offsets, int64_t n,
                          int32_t* ops, int64_t ops_cap, int64_t* offsets, int32_t* status,
                          int64_t* n_words_out);
+/* The same, compiled by n_threads host threads (0 = every hardware thread); identical
+ * output.  Replaces the per-candidate sympify of the worker (:1767) at the rate one GPU
+ * validates.                                                                              */
+int pdeval_compile_batch_mt(int problem_id, const char* text, const int64_t* str_offsets, int64_t n,
+                            int32_t* ops, int64_t ops_cap, int64_t* offsets, int32_t* status,
+                            int64_t* n_words_out, int n_threads);
+/* The reference's reason strings of n validated candidates (host only, pdreasons.cpp), as
+ * validate() returns them (problems/force_free/validator.py:309-427 "Valid foliation ...",
+ * "Invalid (point check ≈ x.xxe±yy)" ...; problems/kerr_magnetosphere/validator.py:231-323),
+ * the same texts as pdeval/batch.py::reason_for, newline-separated into buf[0 .. *len_out).
+ * rational[i] != 0: det at p* is a rational Number (header PDEVAL_FLAG_RATIONAL).  An
+ * UNSUPPORTED row reads "Error: unsupported construct (opcode)".  Returns PDEVAL_ERR_ARG
+ * (and *len_out = -1) when cap bytes are not enough.                                       */
+int pdeval_format_reasons(int problem_id, int64_t n, const uint8_t* status, const double* res_ref,
+                          int n_ref, const double* q_ref, const double* q_grid, const uint8_t* rational,
+                          char* buf, int64_t cap, int64_t* len_out);
 /* Canonical form of the evaluated expression tree of one string (parity tests against
  * SymPy's tree): returns a PDEVAL_COMPILE_* status, or -1 on a bad argument / small buffer. */
 int pdeval_canonical(int problem_id, const char* s, int64_t len, char* out, int64_t cap);

@@ -236,7 +236,7 @@ static void kerr_terms(double r, double x, const double complex* c, int cplx, do
 
 typedef struct {
     double res_abs, res_re, scale;
-    int finite, grad_zero;
+    int finite, grad_zero, tiny;
     double u0;
     double noise;   /* tier 2 only: first-order rounding-noise bound of the residual */
     double grad[2], grad_err[2];   /* quad tier: |u_x|, |u_y| and their error bounds (EPSQ units) */
@@ -360,6 +360,14 @@ static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, 
     r.res_abs = (double)cabsq(res);
     r.res_re = (double)crealq(res);
     r.finite = fin && finiteq(crealq(res)) && finiteq(cimagq(res)) && isfinite(r.scale) && isfinite(r.noise);
+    if (problem != PDEVAL_PROBLEM_FORCE_FREE) {
+        /* Kerr: every coefficient below 2^-900 (kTinyJet, pdeval_kernels.h) -- u underflowed in
+         * the device's fp64; the reference's N(lhs, 40) finds |lhs| astronomically small: a
+         * passing point that decides nothing else */
+        int tiny = 1;
+        for (int i = 0; i < NC(K); ++i) tiny = tiny && cabsq(cq[i]) < 0x1p-900Q && !(W[i] >= 0x1p-900);
+        if (tiny) { r.finite = 1; r.tiny = 1; }
+    }
     r.grad_zero = cq[IDX(1, 0)] == 0 && cq[IDX(0, 1)] == 0;
     r.grad[0] = (double)cabsq(cq[IDX(1, 0)]);
     r.grad[1] = (double)cabsq(cq[IDX(0, 1)]);
@@ -377,8 +385,12 @@ static int kerr_constant_test(const int32_t* w, int64_t nw, double kappa) {
         __complex128 cq[NCMAX];
         double W[NCMAX];
         if (run_q(w, nw, (__float128)kCtX[p], (__float128)kCtY[p], 2, 0, cq, W, 0.0, KC.prm_g_q)) return 0;
-        for (int i = 0; i < NC(2); ++i)
+        int tiny = 1;
+        for (int i = 0; i < NC(2); ++i) {
             if (!(fabsq(crealq(cq[i])) < 0x1p160Q)) return 0;
+            tiny = tiny && cabsq(cq[i]) < 0x1p-900Q && !(W[i] >= 0x1p-900);
+        }
+        if (tiny) return 0;   /* an underflowed jet is no evidence of a constant */
         if ((double)cabsq(cq[IDX(1, 0)]) > kappa * (double)EPSQ * W[IDX(1, 0)]) return 0;
         if ((double)cabsq(cq[IDX(0, 1)]) > kappa * (double)EPSQ * W[IDX(0, 1)]) return 0;
     }
@@ -403,7 +415,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
         int64_t nw = offsets[ci + 1] - offsets[ci];
         int cls = -1, cplx = 0;
         double qr = 0, qmax = 0;
-        int nb = 0, nnf = 0, nfin = 0, any_grad = 0, point_reject = 0, gconst = 1;
+        int nb = 0, nnf = 0, nfin = 0, any_grad = 0, point_reject = 0, gconst = 1, point_nz = 0;
         if (nw < 2 || (w[0] & 0xff) != 0) cls = PDEVAL_CLS_BAD_PROGRAM;
         const uint32_t hdr = nw > 0 ? (uint32_t)w[0] : 0u;
         if (cls < 0 && (hdr & PDEVAL_FLAG_COMPLEX)) {
@@ -411,7 +423,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
             else cls = PDEVAL_CLS_REJECT_POINT;                   /* Kerr: non-real at a test point */
         }
     again:
-        qr = 0; qmax = 0; nb = nnf = nfin = any_grad = point_reject = 0; gconst = 1;
+        qr = 0; qmax = 0; nb = nnf = nfin = any_grad = point_reject = point_nz = 0; gconst = 1;
         for (int p = 0; p < npts && cls < 0; ++p) {
             int rc;
             pt_result r = eval_point(problem, w, nw, px[p], py[p], cplx, 0, &rc, p >= nref);
@@ -424,7 +436,9 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                 /* the point stage, in quad precision (validator.py:349-402 / kerr :163-192):
                  * force-free rejects a residual that is certainly non-zero (beyond kappa x
                  * its noise bound) when it is rational (an exact Number != 0) or >= 1e-20;
-                 * Kerr rejects max |lhs| >= 1e-10 */
+                 * Kerr rejects max |lhs| >= 1e-10.  A residual certainly non-zero but below the
+                 * threshold passes the point stage, but then the symbolic stage cannot reduce it
+                 * to 0 (validator.py:404-427, kerr :283-315): point_nz */
                 int rcq;
                 pt_result q = eval_point_q(problem, w, nw, p, cplx, &rcq);
                 if (rcq == -2 || rcq == -3) { cls = PDEVAL_CLS_UNSUPPORTED; break; }
@@ -433,7 +447,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                 if (res_ref) res_ref[ci * nref + p] = copysign(q.res_abs, q.res_re);
                 /* Kerr constant exclusion (kerr validator.py:231-240: simplify(u) has neither r
                  * nor x): at every reference point the gradient is within its rounding bound */
-                gconst = gconst && q.finite &&
+                gconst = gconst && q.finite && !q.tiny &&
                          q.grad[0] <= prm->noise_kappa * (double)EPSQ * q.grad_err[0] &&
                          q.grad[1] <= prm->noise_kappa * (double)EPSQ * q.grad_err[1];
                 if (!q.finite) {
@@ -441,12 +455,15 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                     point_reject = 1;    /* non-finite at a reference point: final */
                 } else if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
                     qr = scaled(q.res_abs, q.scale);
-                    if (q.res_abs > prm->noise_kappa * q.noise &&
-                        ((hdr & PDEVAL_FLAG_RATIONAL) || q.res_abs >= prm->point_abs_tol))
-                        point_reject = 1;
+                    if (q.res_abs > prm->noise_kappa * q.noise) {
+                        if ((hdr & PDEVAL_FLAG_RATIONAL) || q.res_abs >= prm->point_abs_tol) point_reject = 1;
+                        else point_nz = 1;
+                    }
                 } else {
                     if (!(qr >= q.res_abs)) qr = q.res_abs;
-                    if (q.res_abs >= prm->kerr_abs_tol) point_reject = 1;
+                    if (q.tiny) { /* underflowed: a passing point */ }
+                    else if (q.res_abs >= prm->kerr_abs_tol) point_reject = 1;
+                    else if (q.res_abs > prm->noise_kappa * q.noise) point_nz = 1;
                 }
                 if (p == nref - 1 && point_reject && !prm->full_grid) cls = PDEVAL_CLS_REJECT_POINT;
                 continue;
@@ -474,8 +491,10 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
         }
         if (cls < 0) {
             int structural = problem != PDEVAL_PROBLEM_FORCE_FREE || (hdr & PDEVAL_FLAG_NOCOORD);
-            const int pconst = problem != PDEVAL_PROBLEM_FORCE_FREE && gconst &&
-                               kerr_constant_test(w, nw, prm->noise_kappa);
+            /* Kerr: no coordinate in the program is a constant structurally (kerr validator.py:
+             * 231-240), else the numeric constant test */
+            const int pconst = problem != PDEVAL_PROBLEM_FORCE_FREE &&
+                               ((hdr & PDEVAL_FLAG_NOCOORD) || (gconst && kerr_constant_test(w, nw, prm->noise_kappa)));
             if (pconst) any_grad = 0;
             if (!any_grad && (nfin > 0 || pconst) && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;
             else if (point_reject) cls = PDEVAL_CLS_REJECT_POINT;
@@ -484,6 +503,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
             else if (nb > prm->max_bad) cls = PDEVAL_CLS_REJECT_GRID;
             else if (problem == PDEVAL_PROBLEM_FORCE_FREE && prm->strict_symbolic &&
                      (hdr & (PDEVAL_FLAG_NONSMOOTH2D | PDEVAL_FLAG_UNPROVABLE))) cls = PDEVAL_CLS_REJECT_SYMBOLIC;
+            else if (point_nz) cls = PDEVAL_CLS_REJECT_GRID;   /* residual != 0 identically */
             else cls = PDEVAL_CLS_ACCEPT;
         }
         if (status) status[ci] = (uint8_t)cls;

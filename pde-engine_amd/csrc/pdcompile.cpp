@@ -28,10 +28,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <deque>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -1296,6 +1298,66 @@ int pdeval_compile_batch(int problem_id, const char* text, const int64_t* str_of
         }
         status[i] = st;
         offsets[i + 1] = pos;   // declined / unparsable strings get an empty slot
+    }
+    if (n_words_out) *n_words_out = pos;
+    return PDEVAL_OK;
+}
+
+// The same over a pool of host threads: the batch is cut into chunks that the threads claim
+// from a shared counter (candidates differ in cost), each chunk compiled into its own buffer by
+// its own Ctx (the compiler keeps no global state), then the chunks are laid out in order.
+// Output identical to pdeval_compile_batch.
+int pdeval_compile_batch_mt(int problem_id, const char* text, const int64_t* str_offsets, int64_t n,
+                            int32_t* ops, int64_t ops_cap, int64_t* offsets, int32_t* status,
+                            int64_t* n_words_out, int n_threads) {
+    const SymInfo* syms;
+    int nsyms;
+    if (!problem_syms(problem_id, &syms, &nsyms) || n < 0 || (n > 0 && (!text || !str_offsets)) ||
+        !offsets || !status)
+        return PDEVAL_ERR_ARG;
+    if (n_threads <= 0) n_threads = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int64_t kChunk = 512;
+    const int64_t n_chunks = (n + kChunk - 1) / kChunk;
+    if (n_threads > n_chunks) n_threads = (int)std::max<int64_t>(1, n_chunks);
+    if (n_threads <= 1) return pdeval_compile_batch(problem_id, text, str_offsets, n, ops, ops_cap, offsets,
+                                                    status, n_words_out);
+    for (int64_t i = 0; i < n; ++i)
+        if (str_offsets[i] < 0 || str_offsets[i + 1] < str_offsets[i]) return PDEVAL_ERR_ARG;
+    std::vector<std::vector<int32_t>> words((size_t)n_chunks);
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+        Ctx C;
+        std::vector<int32_t> prog;
+        for (;;) {
+            const int64_t ch = next.fetch_add(1);
+            if (ch >= n_chunks) break;
+            const int64_t lo = ch * kChunk, hi = std::min(n, lo + kChunk);
+            std::vector<int32_t>& w = words[(size_t)ch];
+            for (int64_t i = lo; i < hi; ++i) {
+                const int64_t b = str_offsets[i], e = str_offsets[i + 1];
+                const int st = compile_one(C, syms, nsyms, text + b, (size_t)(e - b), prog, nullptr);
+                status[i] = st;
+                if (st == 0) w.insert(w.end(), prog.begin(), prog.end());
+                offsets[i + 1] = (int64_t)w.size();   // chunk-relative end, rebased below
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < n_threads; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    int64_t pos = 0;
+    offsets[0] = 0;
+    for (int64_t ch = 0; ch < n_chunks; ++ch) {
+        const std::vector<int32_t>& w = words[(size_t)ch];
+        if (pos + (int64_t)w.size() > ops_cap) {
+            if (n_words_out) *n_words_out = -1;   // buffer too small
+            return PDEVAL_ERR_ARG;
+        }
+        if (!w.empty()) memcpy(ops + pos, w.data(), w.size() * sizeof(int32_t));
+        const int64_t lo = ch * kChunk, hi = std::min(n, lo + kChunk);
+        for (int64_t i = lo; i < hi; ++i) offsets[i + 1] += pos;
+        pos += (int64_t)w.size();
     }
     if (n_words_out) *n_words_out = pos;
     return PDEVAL_OK;

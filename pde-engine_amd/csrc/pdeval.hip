@@ -757,8 +757,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         b.cplx_count = cnt + L_DDC;
         b.esc_list = c->d_list[L_DD8];
         b.esc_count = cnt + L_DD8;
-        hipLaunchKernelGGL(dd_collect_kernel<PROB>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b,
-                           (const uint8_t*)a.out.status);
+        hipLaunchKernelGGL(dd_collect_kernel<PROB>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
         HIPCHK(c, hipGetLastError());
         launch_dd_point(PROB, 0, lgrid, s, follow(L_DD, -1, L_ESC));
         launch_dd_point(PROB, 1, lgrid, s, follow(L_DD8, -1, L_ESC));

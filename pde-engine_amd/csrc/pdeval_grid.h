@@ -125,6 +125,15 @@ template <int K, int W, int MAXD> struct Lean {
             const uint32_t wn = rd_word(prog + (more ? npc : pc));
             const int pn = (int)((w >> 8) & 0xffu);   // POWN exponent / coordinate power n
             const bool on_y = (w >> 16) & 1u;         // coordinate-power axis
+            // peephole superinstructions (no change to the program format): PUSH_C c followed
+            // by MUL_P / MUL_X / MUL_Y pushes c * v^n (c * x, c * y) in one dispatch -- set the
+            // coordinate jet and scale it by c, the same products the two opcodes form on a
+            // constant jet; NEG followed by ADDC is c - t.  Kerr programs are 14 % PUSH_C+MUL_*
+            // pairs, force-free 5 % NEG+ADDC.
+            const uint32_t opn = wn & 0xffu;
+            const bool fuse = more && ((op == PDOP_PUSH_C && (opn == PDOP_MUL_P || opn == PDOP_MUL_X ||
+                                                              opn == PDOP_MUL_Y)) ||
+                                       (op == PDOP_NEG && opn == PDOP_ADDC));
             // dispatch: a tree of wave-uniform bit tests over opcode groups (most frequent
             // first), each a structured if/else -- a flat switch lowers to a compare tree whose
             // unstructured joins the structurizer turns into extra flow masks and copies
@@ -153,8 +162,40 @@ template <int K, int W, int MAXD> struct Lean {
                     for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
                 } else {
                     const double c = rd_immp(prog + pc + 1, w, P);
+                    if (!fuse) {
 #pragma unroll
-                    for (int q = 0; q < W; ++q) O::set_const(acc[q], c);
+                        for (int q = 0; q < W; ++q) O::set_const(acc[q], c);
+                    } else if (opn == PDOP_MUL_X) {
+#pragma unroll
+                        for (int q = 0; q < W; ++q) {
+                            O::set_var(acc[q], x[q], 0);
+                            O::scale(acc[q], c);
+                        }
+                    } else if (opn == PDOP_MUL_Y) {
+#pragma unroll
+                        for (int q = 0; q < W; ++q) {
+                            O::set_var(acc[q], y, 1);
+                            O::scale(acc[q], c);
+                        }
+                    } else {
+                        const int pn2 = (int)((wn >> 8) & 0xffu);
+                        double pk[K + 1];
+                        if ((wn >> 16) & 1u) {
+                            O::pcoefs(y, pn2, pk);
+#pragma unroll
+                            for (int q = 0; q < W; ++q) {
+                                O::template set_p<1>(acc[q], pk);
+                                O::scale(acc[q], c);
+                            }
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < W; ++q) {
+                                O::pcoefs(x[q], pn2, pk);
+                                O::template set_p<0>(acc[q], pk);
+                                O::scale(acc[q], c);
+                            }
+                        }
+                    }
                 }
             } else if (b & kCheapMask) {
                 if (op == PDOP_ADDC) {
@@ -164,6 +205,11 @@ template <int K, int W, int MAXD> struct Lean {
                 } else if (op == PDOP_NEG) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], -1.0);
+                    if (fuse) {   // ... ADDC c
+                        const double c = rd_immp(prog + npc + 1, wn, P);
+#pragma unroll
+                        for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
+                    }
                 } else if (op == PDOP_MULC) {
                     const double c = rd_immp(prog + pc + 1, w, P);
 #pragma unroll
@@ -243,10 +289,18 @@ template <int K, int W, int MAXD> struct Lean {
                     else absj<K>(acc[q]);
                 }
             }
-            if (!more) break;
+            int pc_next = npc;
+            uint32_t w_next = wn;
+            bool more_next = more;
+            if (fuse) {   // skip the fused second opcode (ADDC carries an immediate)
+                pc_next = npc + (opn == PDOP_ADDC ? ((wn & PDEVAL_IMM_DD) ? 5 : 3) : 1);
+                more_next = pc_next < plen;
+                w_next = rd_word(prog + (more_next ? pc_next : pc));
+            }
+            if (!more_next) break;
             first = false;
-            pc = npc;
-            w = wn;
+            pc = pc_next;
+            w = w_next;
         }
     }
 

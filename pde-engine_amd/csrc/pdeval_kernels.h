@@ -100,16 +100,20 @@ enum : uint32_t {
 // Point-stage state per candidate (pdeval_point.h).  Bits 0-1: P0_NONE (not decided: malformed
 // program, the grid pass runs its own chunk 0), P0_PASS, P0_REJECT (final).  Flags:
 //   P0_CPLX  not real at the reference point: the complex passes take the candidate
-//   P0_PROV  passed provisionally (|res| within kappa x fp64 noise): if the grid rejects, the
-//            double-double tier re-decides the point stage (REJECT_POINT vs REJECT_GRID)
+//   P0_PROV  passed provisionally (|res| within kappa x fp64 noise): if the grid accepts or
+//            rejects, the double-double tier re-decides the point stage (it may be a REJECT_POINT)
 //   P0_GRAD  a reference point has a non-zero gradient
 //   P0_DD    undecided in fp64 (value too close to its noise or to a threshold): treated as
 //            PASS by the grid passes, decided by the double-double tier at the end
 //   P0_CONST (Kerr) u is constant: at every reference point its gradient lies within the
 //            error bound of its rounding (kerr validator.py:231-240 drops u when simplify(u) has
 //            neither r nor x; a constant's computed gradient is rounding noise, never exactly 0)
+//   P0_NZ    a reference point's residual is CERTAINLY non-zero (beyond kappa x its noise bound)
+//            yet below the point stage's threshold: the residual is not identically zero, so the
+//            reference's symbolic stage cannot reduce it to 0 (force-free validator.py:404-427,
+//            Kerr :283-315) and a grid ACCEPT becomes REJECT_GRID (dd_collect / dd_point)
 enum : uint8_t { P0_NONE = 0, P0_PASS = 1, P0_REJECT = 2, P0_CPLX = 4, P0_PROV = 8, P0_GRAD = 16,
-                 P0_DD = 32, P0_CONST = 64 };
+                 P0_DD = 32, P0_CONST = 64, P0_NZ = 128 };
 
 #define PD_ESC_SHIFT 48
 #define PD_ESC_CAND_MASK ((1ll << PD_ESC_SHIFT) - 1)
@@ -479,6 +483,20 @@ template <int K> __device__ __forceinline__ void absj(typename JetOps<cdd, K>::J
 // residual is then free of intermediate overflow in any evaluation order (force-free S is of
 // degree 6 in the coefficients), so the device and the oracle agree on which points exist.
 constexpr double kHugeJet = 0x1p160;
+// Kerr reference points: a jet whose every coefficient AND every rounding bound is below 2^-900
+// (or a bound that is not finite: 0 * inf in the bound of an underflowed base) has underflowed,
+// e.g. exp_neg(exp(r/a**2)) at a = 1/10.  The reference's N(lhs, 40) has no exponent limit and
+// finds |lhs| astronomically small there, so such a point PASSES the fast point check
+// (kerr validator.py:163-192) and is no evidence of a constant (the constant test, :231-240, is
+// structural: exp(-exp(r/a**2)) has r).  A u that cancels exactly (-x/(1 - x) - 1 + 1/(1 - x))
+// has zero coefficients too, but rounding bounds of the size of its terms: not an underflow.
+constexpr double kTinyJet = 0x1p-900;
+template <class T, int NC> __device__ __forceinline__ bool underflowed(const double* m, const double* e) {
+    bool t = true;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) t = t && m[i] < kTinyJet && !(e[i] >= kTinyJet);
+    return t;
+}
 __device__ __forceinline__ bool jet_coef_ok(double v) { return fabs(v) < kHugeJet; }
 __device__ __forceinline__ bool jet_coef_ok(cplx v) { return fabs(v.re) < kHugeJet && fabs(v.im) < kHugeJet; }
 struct PointResult {

@@ -15,12 +15,14 @@
 //           where |res| <= kappa*noise the point passes PROVISIONALLY (P0_PROV): the exact value
 //           may be 0 (a true solution) or a non-zero hidden in fp64 noise;
 //   tier B (double-double, dd.h, at the end of the call): the undecided candidates (P0_DD) and
-//           the provisional passes whose grid stage rejected -- exactly the candidates whose
-//           class (REJECT_POINT vs REJECT_GRID) depends on the hidden value -- are re-evaluated
-//           with ~106-bit arithmetic, reference points and constants as double-doubles, and
-//           decided for good (noise unit 2^-100).
-// A provisional pass whose grid stage accepts is not re-evaluated: a determinant that vanishes
-// on the whole grid is identically zero (analytic), so it vanishes exactly at p* as well.
+//           every provisional pass that reached a verdict-bearing class (ACCEPT, REJECT_GRID,
+//           REJECT_SYMBOLIC) -- exactly the candidates whose class depends on the hidden value --
+//           are re-evaluated with ~106-bit arithmetic, reference points and constants as
+//           double-doubles, and decided for good (noise unit 2^-100).
+// A provisional pass whose grid stage ACCEPTS is re-evaluated too: the grid accept is a
+// tolerance test (q <= tau_grid), so a non-zero determinant that is below 1e-7 of its magnitude
+// shadow on the whole grid would pass it, while the reference rejects it at p* (an exact
+// non-zero Number, or |det| >= 1e-20).  Accepts are a minority of a batch, so this is cheap.
 // Kernels (launch order in pdeval.hip):
 //   point_kernel         pass 0: all candidates of stack <= 2, real, one candidate per lane
 //   point_list_kernel    deeper real programs (list), then the complex candidates (list)
@@ -66,6 +68,7 @@ struct PtEval {
     double u0;                       // Re u at the point (fingerprint)
     bool finite, grad_zero;
     bool grad_noise;                 // |u_x|, |u_y| within kappa x their rounding-error bounds
+    bool tiny;                       // Kerr: u's jet underflowed (kTinyJet): a passing point
     int rc;                          // RUN_*
 };
 
@@ -121,6 +124,13 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
 #pragma unroll
     for (int i = 0; i < NC; ++i) fin = fin && m[i] < kHugeJet;
     r.finite = fin;
+    if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
+        if (underflowed<T, NC>(m, e)) {
+            r.tiny = true;
+            r.finite = true;
+            r.grad_noise = false;
+        }
+    }
     return r;
 }
 
@@ -150,15 +160,18 @@ __device__ __forceinline__ bool kerr_constant_test(const KernelArgs& a, const in
             m[i] = mag(u.c[i]);
             fin = fin && m[i] < kHugeJet;
         }
-        if (!fin || m[ji(1, 0)] > gk * e[ji(1, 0)] || m[ji(0, 1)] > gk * e[ji(0, 1)]) return false;
+        // an underflowed jet is no evidence of a constant
+        if (!fin || underflowed<T, NC>(m, e) || m[ji(1, 0)] > gk * e[ji(1, 0)] || m[ji(0, 1)] > gk * e[ji(0, 1)])
+            return false;
     }
     return true;
 }
 
 // ---- decision rules.  FINAL = the double-double tier (nothing is left undecided).
-// Force-free (validator.py:371-397): returns P0_PASS / P0_REJECT, | P0_PROV, | P0_DD.
+// Force-free (validator.py:371-397): returns P0_PASS / P0_REJECT, | P0_PROV, | P0_DD, | P0_NZ.
 // P0_DD alone with P0_PASS: the class is undecided in fp64 (the grid passes treat it as passed);
 // P0_DD with a decided class: only the reported residual needs the double-double value.
+// P0_NZ with P0_PASS: certainly non-zero but below 1e-20 (not a solution: det is not == 0).
 template <bool FINAL>
 __device__ __forceinline__ uint8_t ff_point_rule(double res_abs, double noise, bool rational,
                                                  const pdeval_params& prm) {
@@ -169,22 +182,24 @@ __device__ __forceinline__ uint8_t ff_point_rule(double res_abs, double noise, b
         const uint8_t acc = (!FINAL && noise > prm.res_rel_acc * res_abs) ? P0_DD : 0;
         if (rational) return P0_REJECT | acc;             // an exact Number != 0
         if (res_abs - kn >= prm.point_abs_tol) return P0_REJECT | acc;   // |evalf(50)| >= 1e-20
-        if (res_abs + kn < prm.point_abs_tol) return P0_PASS | acc;      // non-zero below 1e-20
+        if (res_abs + kn < prm.point_abs_tol) return P0_PASS | P0_NZ | acc;   // non-zero below 1e-20
         if (!FINAL) return P0_DD | P0_PASS;
-        return res_abs >= prm.point_abs_tol ? P0_REJECT : P0_PASS;
+        return res_abs >= prm.point_abs_tol ? P0_REJECT : (uint8_t)(P0_PASS | P0_NZ);
     }
     return FINAL ? P0_PASS : (uint8_t)(P0_PASS | P0_PROV);
 }
 
 // Kerr, one reference point (kerr validator.py:190, absolute tolerance): 0 pass, 1 reject,
-// 2 undecided in fp64; | 4: the value is not accurate enough to report (double-double value).
+// 2 undecided in fp64; | 4: the value is not accurate enough to report (double-double value);
+// | 8: the value is certainly non-zero (beyond kappa x its noise bound).
 template <bool FINAL>
 __device__ __forceinline__ int kerr_point_rule(double res_abs, double noise, const pdeval_params& prm) {
     const double kn = prm.noise_kappa * noise;
-    if (FINAL) return res_abs >= prm.kerr_abs_tol ? 1 : 0;
+    const int nz = res_abs > kn ? 8 : 0;
+    if (FINAL) return (res_abs >= prm.kerr_abs_tol ? 1 : 0) | nz;
     const int acc = (res_abs > kn && noise > prm.res_rel_acc * res_abs) ? 4 : 0;
-    if (res_abs - kn >= prm.kerr_abs_tol) return 1 | acc;
-    if (res_abs + kn < prm.kerr_abs_tol) return 0 | acc;
+    if (res_abs - kn >= prm.kerr_abs_tol) return 1 | acc | nz;
+    if (res_abs + kn < prm.kerr_abs_tol) return 0 | acc | nz;
     return 2;
 }
 
@@ -195,7 +210,7 @@ template <int PROB, class T, class V, int MAXD, bool VEC, bool FINAL, class STK>
 __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand, const int32_t* prog, int plen,
                                                uint32_t hdr, STK& stk, bool* nonfinite, bool* prog_err) {
     double qr = 0.0;
-    bool nf = false, grad = false, rej = false, und = false, inacc = false, gconst = true;
+    bool nf = false, grad = false, rej = false, und = false, inacc = false, gconst = true, nzk = false;
     uint8_t ff = P0_PASS;
     *prog_err = false;
     for (int p = 0; p < a.n_ref; ++p) {
@@ -223,10 +238,12 @@ __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand
             ff = ff_point_rule<FINAL>(r.res_abs, r.noise, (hdr & PDEVAL_FLAG_RATIONAL) != 0, a.prm);
         } else {
             qr = fmax(qr, r.res_abs);
+            if (r.tiny) continue;   // underflowed: |lhs| far below the threshold
             const int k = kerr_point_rule<FINAL>(r.res_abs, r.noise, a.prm);
             rej = rej || (k & 3) == 1;
             und = und || (k & 3) == 2;
             inacc = inacc || (k & 4);
+            nzk = nzk || (k & 8);
         }
     }
     *nonfinite = nf;
@@ -235,10 +252,15 @@ __device__ __forceinline__ uint8_t point_stage(const KernelArgs& a, int64_t cand
     if (nf) ps = P0_REJECT;    // Kerr: non-real / NaN at a test point; FF complex: not finite
     else if (PROB == PDEVAL_PROBLEM_FORCE_FREE) ps = ff;
     else ps = und ? (uint8_t)(P0_DD | P0_PASS) : (rej ? P0_REJECT : P0_PASS);
+    if (PROB != PDEVAL_PROBLEM_FORCE_FREE && nzk && !nf && !rej) ps |= P0_NZ;
     if (inacc) ps |= P0_DD;
     if (grad) ps |= P0_GRAD;
     if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
-        if (gconst && kerr_constant_test<PROB, T, V, MAXD, VEC>(a, prog, plen, stk)) ps |= P0_CONST;
+        // a program with no coordinate is a constant structurally (simplify(u) has neither r
+        // nor x); otherwise the numeric constant test
+        if ((hdr & PDEVAL_FLAG_NOCOORD) ||
+            (gconst && kerr_constant_test<PROB, T, V, MAXD, VEC>(a, prog, plen, stk)))
+            ps |= P0_CONST;
     }
     return ps;
 }
@@ -357,18 +379,29 @@ __global__ __launch_bounds__(64, 1) void point_list_kernel(KernelArgs a) {
 }
 
 // Tier-B lists: the candidates whose point stage fp64 left undecided, and the provisional
-// passes whose final class is a grid reject (that class may really be a point reject).
+// passes whose final class is an accept or a grid reject (either may really be a point reject).
+// A point pass certainly non-zero (P0_NZ) that the grid accepted is a REJECT_GRID: the residual
+// is not identically zero (the reference's symbolic stage fails on it).
+__device__ __forceinline__ void nz_reject(const KernelArgs& a, int64_t cand) {
+    a.out.status[cand] = PDEVAL_CLS_REJECT_GRID;
+    if (a.out.verdict_bits) atomicAnd((uint32_t*)a.out.verdict_bits + (cand >> 5), ~(1u << (cand & 31)));
+}
+
 template <int PROB>
-__global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a, const uint8_t* status) {
+__global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a) {
     const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= a.n) return;
     const int64_t cand = a.perm ? (int64_t)a.perm[li] : li;   // lists in shape order
     const uint8_t ps = a.pstate[cand];
     if ((ps & 3) == P0_NONE) return;
-    const uint8_t st = status[cand];
+    const uint8_t st = a.out.status[cand];
     const bool need = (ps & P0_DD) ||
-                      ((ps & P0_PROV) && (st == PDEVAL_CLS_REJECT_GRID || st == PDEVAL_CLS_REJECT_SYMBOLIC));
-    if (!need) return;
+                      ((ps & P0_PROV) && (st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||
+                                            st == PDEVAL_CLS_REJECT_SYMBOLIC));
+    if (!need) {
+        if ((ps & 3) == P0_PASS && (ps & P0_NZ) && st == PDEVAL_CLS_ACCEPT) nz_reject(a, cand);
+        return;
+    }
     if (ps & P0_CPLX) {
         list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
     } else {
@@ -505,7 +538,7 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
     constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
     constexpr int NC = nc(K);
     double qr = 0.0;
-    bool rej = false, fin_all = true;
+    bool rej = false, fin_all = true, nzk = false;
     uint8_t ff = P0_PASS;
     for (int p = 0; p < a.n_ref; ++p) {
         const dd x = a.ref_xd[p & 3], y = a.ref_yd[p & 3];
@@ -524,6 +557,16 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
         }
         const double res_abs = mag(res);
         const double noise = a.noise_ref[cand * a.n_ref + p] * (dd_unit() / kEps);
+        if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
+            bool tiny = true;
+#pragma unroll
+            for (int i = 0; i < NC; ++i) tiny = tiny && m[i] < kTinyJet;
+            if (tiny) {   // underflowed: a passing point (kTinyJet)
+                if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = re_hi(res);
+                qr = fmax(qr, res_abs);
+                continue;
+            }
+        }
         bool fin = finite_(res) && isfinite(S) && isfinite(noise);
 #pragma unroll
         for (int i = 0; i < NC; ++i) fin = fin && m[i] < kHugeJet;
@@ -539,7 +582,9 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
             ff = ff_point_rule<true>(res_abs, noise, (hdr & PDEVAL_FLAG_RATIONAL) != 0, a.prm);
         } else {
             qr = fmax(qr, res_abs);
-            rej = rej || kerr_point_rule<true>(res_abs, noise, a.prm) == 1;
+            const int k = kerr_point_rule<true>(res_abs, noise, a.prm);
+            rej = rej || (k & 3) == 1;
+            nzk = nzk || (k & 8);
         }
     }
     // Kerr: a reference point where even the double-double value is not finite is a pole (or
@@ -547,8 +592,8 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
     // reject either way (kerr validator.py:178-190).  Force-free keeps the fp64 decision.
     if (!fin_all) return PROB == PDEVAL_PROBLEM_FORCE_FREE ? P0_NONE : P0_REJECT;
     if (a.out.q_ref) a.out.q_ref[cand] = qr;
-    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) return ff & 3;
-    else return rej ? P0_REJECT : P0_PASS;
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) return ff & (3 | P0_NZ);
+    else return rej ? P0_REJECT : (uint8_t)(nzk ? P0_PASS | P0_NZ : P0_PASS);
 }
 
 // Tier B: the point stage in double-double (T = dd, or cdd for complex candidates), final,
@@ -586,8 +631,10 @@ __global__ __launch_bounds__(64, MAXD == 2 ? 2 : 1) void dd_point_kernel(KernelA
             write_point_reject(a, cand);
             if (a.out.verdict_bits)
                 atomicAnd((uint32_t*)a.out.verdict_bits + (cand >> 5), ~(1u << (cand & 31)));
+        } else if ((s & 3) == P0_PASS && (s & P0_NZ) && st == PDEVAL_CLS_ACCEPT) {
+            nz_reject(a, cand);
         }
-        a.pstate[cand] = (uint8_t)((a.pstate[cand] & ~(3 | P0_DD | P0_PROV)) | (s & 3));
+        a.pstate[cand] = (uint8_t)((a.pstate[cand] & ~(3 | P0_DD | P0_PROV | P0_NZ)) | s);
     }
 }
 

@@ -25,7 +25,8 @@ EXPORTS = (
     'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts', 'pdeval_eval_points',
     'pdeval_compile_batch', 'pdeval_canonical', 'pdeval_point_eval', 'pdeval_point_states',
     'pdeval_comm_unique_id', 'pdeval_comm_init', 'pdeval_gather_bits', 'pdeval_comm_destroy',
-    'pdeval_default_kerr_constants', 'pdeval_set_kerr_constants',
+    'pdeval_default_kerr_constants', 'pdeval_set_kerr_constants', 'pdeval_compile_batch_mt',
+    'pdeval_format_reasons',
 )
 MAX_BATCH = 1 << 30          # PDEVAL_MAX_BATCH
 UNIQUE_ID_BYTES = 128
@@ -97,6 +98,8 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_eval_points.argtypes = [vp, vp, i64, vp, vp, C.c_int, C.c_int, vp, vp]
     lib.pdeval_compile_batch.argtypes = [C.c_int, vp, vp, i64, vp, i64, vp, vp, vp]
     lib.pdeval_canonical.argtypes = [C.c_int, C.c_char_p, i64, C.c_char_p, i64]
+    lib.pdeval_compile_batch_mt.argtypes = [C.c_int, vp, vp, i64, vp, i64, vp, vp, vp, C.c_int]
+    lib.pdeval_format_reasons.argtypes = [C.c_int, i64, vp, vp, C.c_int, vp, vp, vp, vp, i64, vp]
     lib.pdeval_point_eval.argtypes = [vp, vp, i64, C.c_int, vp, vp]
     lib.pdeval_point_states.argtypes = [vp, vp, i64]
     lib.pdeval_comm_unique_id.argtypes = [vp]

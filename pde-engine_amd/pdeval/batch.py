@@ -33,8 +33,8 @@ import sympy as sp
 from . import problem_defs as P
 from .flatten import Unsupported
 from .opcodes import (CLS_ACCEPT, CLS_BAD_PROGRAM, CLS_NONFINITE_REF, CLS_REJECT_GRID,
-                      CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC, CLS_UNSUPPORTED, CLS_ZERO_GRADIENT, FLAG_RATIONAL,
-                      HAS_IMM, IMM_PRM, PROBLEM_FORCE_FREE, PROBLEM_KERR, op_len)
+                      CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC, CLS_UNSUPPORTED, CLS_ZERO_GRADIENT, FLAG_NOCOORD,
+                      FLAG_RATIONAL, HAS_IMM, IMM_PRM, PDOP, PROBLEM_FORCE_FREE, PROBLEM_KERR, op_len)
 
 
 @dataclass
@@ -86,6 +86,47 @@ def reason_for(problem_id: int, cls: int, res_ref: Sequence[float], q_ref: float
     return False, 'Error: malformed program'
 
 
+def rational_flags(ops, off) -> np.ndarray:
+    """Per candidate: header flag PDEVAL_FLAG_RATIONAL (det at p* is a rational Number)."""
+    off = np.asarray(off, dtype=np.int64)
+    if len(off) < 2:
+        return np.zeros(0, dtype=np.uint8)
+    hdr = np.asarray(ops, dtype=np.int32)[np.minimum(off[:-1], max(len(ops) - 1, 0))] if len(ops) else \
+        np.zeros(len(off) - 1, dtype=np.int32)
+    return ((hdr & FLAG_RATIONAL) != 0).astype(np.uint8)
+
+
+def format_reasons(problem_id: int, status, res_ref, q_ref, q_grid, rational,
+                   notes: Optional[Sequence[Optional[str]]] = None) -> List[str]:
+    """reason_for over a whole batch, in one native call (pdeval_format_reasons,
+    csrc/pdreasons.cpp): the same strings, newline-joined by the library and split once here.
+    ``notes[i]`` (UNSUPPORTED stubs) replaces the generic construct name as in reason_for."""
+    import ctypes as C
+    from ._lib import load, PdevalError
+    st = np.ascontiguousarray(status, dtype=np.uint8)
+    n = len(st)
+    if n == 0:
+        return []
+    rr = np.ascontiguousarray(res_ref, dtype=np.float64).reshape(n, -1)
+    qr = np.ascontiguousarray(q_ref, dtype=np.float64)
+    qg = np.ascontiguousarray(q_grid, dtype=np.float64)
+    ra = np.ascontiguousarray(rational, dtype=np.uint8)
+    cap = 112 * n + 64
+    buf = C.create_string_buffer(cap)
+    ln = C.c_int64(0)
+    rc = load().pdeval_format_reasons(problem_id, n, st.ctypes.data, rr.ctypes.data, rr.shape[1],
+                                      qr.ctypes.data, qg.ctypes.data, ra.ctypes.data, buf, cap,
+                                      C.byref(ln))
+    if rc != 0:
+        raise PdevalError(f'pdeval_format_reasons failed ({rc})')
+    out = buf.raw[:ln.value].decode('utf-8').split('\n')
+    if notes is not None:
+        for i in np.flatnonzero(st == CLS_UNSUPPORTED):
+            if notes[i]:
+                out[i] = f'Error: unsupported construct ({notes[i]})'
+    return out
+
+
 def symbolic_zero_gradient(pd, items, out) -> List[int]:
     """Force-free: the reference's zero-gradient test is symbolic -- ``u.diff(rho) == 0 and
     u.diff(z) == 0`` on SymPy's tree (``problems/force_free/validator.py:305-312``).  SymPy can
@@ -117,6 +158,52 @@ def symbolic_zero_gradient(pd, items, out) -> List[int]:
                     out['verdict'][i] = False
                 rows.append(i)
         except Exception:   # noqa: BLE001  (a tree SymPy cannot differentiate keeps its class)
+            pass
+    return rows
+
+
+_NONRATIONAL_OPS = {PDOP['ABS'], PDOP['SQRT'], PDOP['POW'], PDOP['LOG']}
+
+
+def _has_op(words, codes) -> bool:
+    i = 1
+    while i < len(words):
+        w = int(words[i])
+        if (w & 0xff) in codes:
+            return True
+        i += op_len(w)
+    return False
+
+
+def kerr_symbolic_constant(pd, items, out, ops, off) -> List[int]:
+    """Kerr: the reference's constant exclusion is structural -- ``simplify(u)`` has neither r
+    nor x (``problems/kerr_magnetosphere/validator.py:231-240``).  The device decides it
+    numerically (P0_CONST: u's gradient is rounding noise at every constant-test point), which
+    is the same thing for rational and exp combinations, but not for a u that is constant only
+    on the domain through an Abs or a fractional power: ``Delta - sqrt(square(Delta))`` is 0
+    for every r > r+, yet SymPy keeps ``Abs(Delta)`` and the reference goes on to its symbolic
+    stage, which cannot prove lhs == 0 ("PDE residual != 0 | ...").  So the numeric constants
+    whose program has an Abs, sqrt, fractional power or log (and that reference a coordinate;
+    no coordinate is a constant structurally) are re-checked here with the reference's own test
+    and reclassified REJECT_GRID where simplify(u) keeps a coordinate.  Updates ``out`` in
+    place; returns the changed rows."""
+    if pd.problem_id != PROBLEM_KERR:
+        return []
+    st = np.asarray(out['status'])
+    rows = []
+    for i in np.flatnonzero(st == CLS_ZERO_GRADIENT):
+        w = ops[off[i]:off[i + 1]]
+        if len(w) == 0 or int(w[0]) & FLAG_NOCOORD or not _has_op(w, _NONRATIONAL_OPS):
+            continue
+        try:
+            u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
+            us = sp.simplify(u)
+            if us.has(pd.x) or us.has(pd.y):
+                st[i] = CLS_REJECT_GRID
+                if 'verdict' in out:
+                    out['verdict'][i] = False
+                rows.append(i)
+        except Exception:   # noqa: BLE001  (SymPy failed: the device's class stands)
             pass
     return rows
 
@@ -219,22 +306,51 @@ class BatchValidator:
         ops, off, notes = self.compile(exprs)
         return self._verdicts(ops, off, notes, exprs)
 
-    def _verdicts(self, ops, off, notes, items) -> List[Verdict]:
-        r = self.run(ops, off)
+    def host_steps(self, r, ops, off, items):
+        """The host steps every device result goes through (in place): the symbolic
+        zero-gradient re-check (force-free), the structural constant re-check of numeric
+        constants with an Abs or fractional power (Kerr) and, for Kerr at a = 0, the
+        reference's exact point check."""
         symbolic_zero_gradient(self.pd, items, r)
+        kerr_symbolic_constant(self.pd, items, r, ops, off)
         kerr_exact_point_check(self.pd, self.kerr, items, r, ops, off, self.params.kerr_abs_tol,
                                self.ctx.n_points - self.ctx.n_ref)
-        out = []
-        for i in range(len(off) - 1):
-            hdr = int(ops[off[i]])
-            ok, reason = reason_for(self.problem_id, int(r['status'][i]), r['res_ref'][i],
-                                    float(r['q_ref'][i]), float(r['q_grid'][i]),
-                                    bool(hdr & FLAG_RATIONAL), notes[i])
-            out.append(Verdict(ok, reason, int(r['status'][i]), float(r['q_ref'][i]),
-                               tuple(float(v) for v in r['res_ref'][i]), float(r['q_grid'][i]),
-                               int(r['n_bad'][i]), int(r['n_nonfinite'][i]),
-                               tuple(float(v) for v in r['fingerprint'][i])))
-        return out
+        return r
+
+    def table(self, r, ops, off, notes) -> dict:
+        """Device result (after host_steps) -> {'ok': bool array, 'reasons': list of str} plus
+        the raw outputs: the reference's (bool, reason) of every candidate, vectorized."""
+        st = np.asarray(r['status'])
+        reasons = format_reasons(self.problem_id, st, r['res_ref'], r['q_ref'], r['q_grid'],
+                                 rational_flags(ops, off), notes)
+        return {**r, 'ok': st == CLS_ACCEPT, 'reasons': reasons}
+
+    def _verdicts(self, ops, off, notes, items) -> List[Verdict]:
+        r = self.host_steps(self.run(ops, off), ops, off, items)
+        t = self.table(r, ops, off, notes)
+        ok, reasons = t['ok'].tolist(), t['reasons']
+        st, qr, qg = r['status'].tolist(), r['q_ref'].tolist(), r['q_grid'].tolist()
+        rr, fp = r['res_ref'].tolist(), r['fingerprint'].tolist()
+        nb, nn = r['n_bad'].tolist(), r['n_nonfinite'].tolist()
+        return [Verdict(ok[i], reasons[i], st[i], qr[i], tuple(rr[i]), qg[i], nb[i], nn[i], tuple(fp[i]))
+                for i in range(len(st))]
+
+    # ---- the worker's fast path in three phases (pdeval/worker.py pipelines them):
+    # prepare (host threads, GIL released in the native compiler), run (one device call,
+    # GIL released), finish (host steps + vectorized reasons)
+    def prepare_strings(self, strings: Sequence[str]) -> dict:
+        from .native import compile_strings
+        stats: dict = {}
+        ops, off, notes = compile_strings(self.pd, list(strings), stats=stats)
+        return {'strings': list(strings), 'ops': ops, 'off': off, 'notes': notes,
+                'compile_status': stats.get('status')}
+
+    def run_prepared(self, p: dict):
+        return self.run(p['ops'], p['off'])
+
+    def finish(self, p: dict, r) -> dict:
+        r = self.host_steps(r, p['ops'], p['off'], p['strings'])
+        return self.table(r, p['ops'], p['off'], p['notes'])
 
     def validate_strings(self, strings: Sequence[str], stats: Optional[dict] = None) -> List[Verdict]:
         """Candidate strings in: compiled by the native compiler (csrc/pdcompile.cpp), SymPy

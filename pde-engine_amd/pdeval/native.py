@@ -14,6 +14,7 @@ of ``sympify``'s tree) and by verdicts (tests/test_native_compile.py).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -31,12 +32,27 @@ def _pack_text(strings: Sequence[str]) -> Tuple[bytes, np.ndarray]:
     return b''.join(enc), off
 
 
-def compile_native(problem_id: int, strings: Sequence[str]):
+def host_threads() -> int:
+    """Host threads for the native compile: PDEVAL_HOST_THREADS, else OMP_NUM_THREADS (16 on
+    the GPU box, whose os.cpu_count() reports the whole machine), else the affinity mask."""
+    for k in ('PDEVAL_HOST_THREADS', 'OMP_NUM_THREADS'):
+        v = os.environ.get(k, '')
+        if v.isdigit() and int(v) > 0:
+            return min(int(v), 64)
+    try:
+        return max(1, min(len(os.sched_getaffinity(0)), 64))
+    except AttributeError:
+        return max(1, min(os.cpu_count() or 1, 64))
+
+
+def compile_native(problem_id: int, strings: Sequence[str], threads: Optional[int] = None):
     """(ops int32, offsets int64[n+1], status int32[n]) from the C++ compiler alone; declined
-    and unparsable strings get empty slots (status != COMPILE_OK)."""
+    and unparsable strings get empty slots (status != COMPILE_OK).  ``threads`` host threads
+    (pdeval_compile_batch_mt; default host_threads(), 1 = the single-threaded entry point)."""
     lib = load()
     text, soff = _pack_text(strings)
     n = len(strings)
+    nt = host_threads() if threads is None else int(threads)
     cap = 8 * len(text) + 16 * n + 64
     while True:
         ops = np.empty(cap, dtype=np.int32)
@@ -44,9 +60,14 @@ def compile_native(problem_id: int, strings: Sequence[str]):
         st = np.zeros(n, dtype=np.int32)
         nw = C.c_int64(0)
         tb = C.create_string_buffer(text, len(text) + 1)
-        rc = lib.pdeval_compile_batch(problem_id, C.cast(tb, C.c_void_p), soff.ctypes.data, n,
-                                      ops.ctypes.data, cap, off.ctypes.data, st.ctypes.data,
-                                      C.byref(nw))
+        if nt == 1:
+            rc = lib.pdeval_compile_batch(problem_id, C.cast(tb, C.c_void_p), soff.ctypes.data, n,
+                                          ops.ctypes.data, cap, off.ctypes.data, st.ctypes.data,
+                                          C.byref(nw))
+        else:
+            rc = lib.pdeval_compile_batch_mt(problem_id, C.cast(tb, C.c_void_p), soff.ctypes.data, n,
+                                             ops.ctypes.data, cap, off.ctypes.data, st.ctypes.data,
+                                             C.byref(nw), nt)
         if rc == 0:
             return ops[:nw.value], off, st
         if nw.value != -1:
@@ -54,13 +75,14 @@ def compile_native(problem_id: int, strings: Sequence[str]):
         cap *= 2
 
 
-def compile_strings(pd_, strings: Sequence[str], stats: Optional[dict] = None):
+def compile_strings(pd_, strings: Sequence[str], stats: Optional[dict] = None,
+                    threads: Optional[int] = None):
     """Drop-in for ``problem_defs.compile_strings``: native compile, SymPy for the rest.
     Returns (ops, offsets, notes) with notes[i] = None or the reason a program is a stub.
     With a ``stats`` dict, ``stats['status']`` receives the native compiler's per-string
     status (COMPILE_PARSE marks the strings it could not parse)."""
     from .problem_defs import compile_strings as sympy_compile
-    ops, off, st = compile_native(pd_.problem_id, strings)
+    ops, off, st = compile_native(pd_.problem_id, strings, threads)
     host = np.flatnonzero(st != COMPILE_OK)
     if stats is not None:
         stats.update(n=len(strings), native=int(len(strings) - len(host)), host=int(len(host)), status=st)

@@ -9,7 +9,8 @@ snapshot's worker dies on a broken import):
 * parse  : ``sympify(expr_str, locals=UNARY_OPS + symbols + constants)`` (:1703-1714, :1767);
 * verdict: ``problem.validator.validate_batch(us, **kwargs)`` with the kwargs of :1768-1782
            filtered by the validator's signature -- one GPU call per batch instead of one
-           SymPy ``validate`` per candidate;
+           SymPy ``validate`` per candidate; batches are pipelined (``process_batches``: the
+           next batch compiles on host threads while the current one is on the device);
 * tagging: valid rows are matched against ``problem.known_solutions`` (:1783-1798): a grid
            fingerprint pre-filter on the device, then the reference's ``simplify(u - known)
            == 0`` on the host for fingerprint hits only;
@@ -72,12 +73,11 @@ class KnownSolutionTagger:
             return out
         fp = np.asarray(fps) if fps is not None else self.fingerprints(
             [sp.sympify(u, locals=self.locals) if isinstance(u, str) else u for u in us])
-        for i, u in enumerate(us):
-            for k, (ke, name) in enumerate(self.known):
-                a, b = fp[i], self.fps[k]
-                fin = np.isfinite(a) & np.isfinite(b)
-                if fin.sum() < 2 or not np.allclose(a[fin], b[fin], rtol=self.rtol, atol=1e-12):
-                    continue
+        hits = self.fingerprint_hits(fp)
+        for i in np.flatnonzero(hits.any(axis=1)):
+            u = us[i]
+            for k in np.flatnonzero(hits[i]):
+                ke, name = self.known[k]
                 try:
                     ue = sp.sympify(u, locals=self.locals) if isinstance(u, str) else u
                     if sp.simplify(ue - ke) == 0:        # the reference's test, :1791
@@ -86,6 +86,16 @@ class KnownSolutionTagger:
                 except Exception:   # noqa: BLE001
                     pass
         return out
+
+    def fingerprint_hits(self, fp) -> np.ndarray:
+        """(n, n_known) bool: fingerprint i matches known solution k -- at least 2 points
+        finite in both and np.allclose(rtol, atol=1e-12) on those, for all pairs at once."""
+        a = np.asarray(fp, dtype=np.float64).reshape(-1, 1, self.fps.shape[1])
+        b = self.fps.reshape(1, -1, self.fps.shape[1])
+        with np.errstate(invalid='ignore', over='ignore'):
+            fin = np.isfinite(a) & np.isfinite(b)
+            close = np.abs(a - b) <= 1e-12 + self.rtol * np.abs(b)
+        return (fin.sum(axis=2) >= 2) & np.all(close | ~fin, axis=2)
 
 
 def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[str],
@@ -110,47 +120,54 @@ def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[s
         conn.execute('PRAGMA busy_timeout=5000')
     pid = os.getpid()
     done = 0
-    stop = False
-    last_work = time.time()
-    while not stop:
-        claimed: List[Tuple[int, str]] = []
-        if task_queue is not None:
-            try:
-                item = task_queue.get(timeout=0.2)
-                if item is None:
-                    stop = True
-                else:
-                    claimed.append(item)
-                    while len(claimed) < batch_size:
-                        item = task_queue.get_nowait()
-                        if item is None:
-                            stop = True
-                            break
-                        claimed.append(item)
-            except _queue.Empty:
-                pass
-        if not claimed and conn is not None and not stop:
-            cur = conn.execute(f"SELECT id, expression FROM {table_name} "
-                               f"WHERE validation_status = 'pending' LIMIT 50")
-            for expr_id, expr_str in cur.fetchall():
-                c2 = conn.execute(f"UPDATE {table_name} SET validation_status = 'in_progress' "
-                                  f"WHERE id = ? AND validation_status = 'pending'", (expr_id,))
-                if c2.rowcount == 1:
-                    claimed.append((expr_id, expr_str))
-            conn.commit()
-        if not claimed:
-            if idle_exit_s is not None and time.time() - last_work > idle_exit_s:
-                break
-            if not stop:
-                time.sleep(0.2)
-            continue
+
+    def claims():
+        """Claimed batches, as the reference's loop claims them; None when idle (the pipeline
+        then flushes the batch it holds, so no result waits for the next claim)."""
+        stop = False
         last_work = time.time()
-        if result_queue is not None:
-            try:
-                result_queue.put((run_id, pid, 'start', claimed[0][0], claimed[0][1][:120]), timeout=0.5)
-            except Exception:   # noqa: BLE001
-                pass
-        results = process_batch(claimed, validator, kwargs, locs, tagger)
+        while not stop:
+            claimed: List[Tuple[int, str]] = []
+            if task_queue is not None:
+                try:
+                    item = task_queue.get(timeout=0.2)
+                    if item is None:
+                        stop = True
+                    else:
+                        claimed.append(item)
+                        while len(claimed) < batch_size:
+                            item = task_queue.get_nowait()
+                            if item is None:
+                                stop = True
+                                break
+                            claimed.append(item)
+                except _queue.Empty:
+                    pass
+            if not claimed and conn is not None and not stop:
+                cur = conn.execute(f"SELECT id, expression FROM {table_name} "
+                                   f"WHERE validation_status = 'pending' LIMIT 50")
+                for expr_id, expr_str in cur.fetchall():
+                    c2 = conn.execute(f"UPDATE {table_name} SET validation_status = 'in_progress' "
+                                      f"WHERE id = ? AND validation_status = 'pending'", (expr_id,))
+                    if c2.rowcount == 1:
+                        claimed.append((expr_id, expr_str))
+                conn.commit()
+            if not claimed:
+                if idle_exit_s is not None and time.time() - last_work > idle_exit_s:
+                    break
+                yield None
+                if not stop:
+                    time.sleep(0.2)
+                continue
+            last_work = time.time()
+            if result_queue is not None:
+                try:
+                    result_queue.put((run_id, pid, 'start', claimed[0][0], claimed[0][1][:120]), timeout=0.5)
+                except Exception:   # noqa: BLE001
+                    pass
+            yield claimed
+
+    for results in process_batches(claims(), validator, kwargs, locs, tagger):
         done += len(results)
         if result_queue is not None:
             result_queue.put((run_id, pid, 'end', results), timeout=5.0)
@@ -190,25 +207,75 @@ def _process_batch_strings(claimed, validator, locs, tagger):
     from that call's fingerprints -- SymPy parses only parse errors (whose message the
     reference reports as 'Validator Error: ...', :1703-1714) and fingerprint hits (the
     reference's simplify(u - known) == 0, :1785-1798)."""
-    from .native import COMPILE_PARSE
     bv = validator._validator()
-    strs = [s for _, s in claimed]
-    stats: dict = {}
-    verdicts = bv.validate_strings(strs, stats=stats)
-    st = stats.get('status')
-    results, keep = [], []
-    for i, (expr_id, expr_str) in enumerate(claimed):
-        if st is not None and st[i] == COMPILE_PARSE:
+    p = bv.prepare_strings([s for _, s in claimed])
+    return _results(claimed, p, bv.finish(p, bv.run_prepared(p)), locs, tagger)
+
+
+def _results(claimed, p, t, locs, tagger):
+    """Result tuples of one batch from its compile (p) and its verdict table (t): errors
+    first, then the completed rows in claim order (the order process_batch has always used)."""
+    from itertools import repeat
+    from .native import COMPILE_PARSE
+    cst = p.get('compile_status')
+    ok, reasons = t['ok'], t['reasons']
+    ids = [e for e, _ in claimed]
+    results = []
+    drop = np.zeros(len(claimed), dtype=bool)
+    if cst is not None:
+        for i in np.flatnonzero(np.asarray(cst) == COMPILE_PARSE):
             try:
-                sp.sympify(expr_str, locals=locs)
+                sp.sympify(claimed[i][1], locals=locs)
             except Exception as e:   # noqa: BLE001
-                results.append(('error', None, f'Validator Error: {e}', None, None, expr_id))
-                continue
-        keep.append(i)
-    valid = [i for i in keep if verdicts[i].ok]
-    tags = dict(zip(valid, tagger.tag([strs[i] for i in valid],
-                                      fps=np.array([verdicts[i].fingerprint for i in valid]).reshape(-1, 4))))
-    for i in keep:
-        is_paper, name = tags.get(i, (False, None))
-        results.append(('completed', bool(verdicts[i].ok), verdicts[i].reason, is_paper, name, claimed[i][0]))
+                results.append(('error', None, f'Validator Error: {e}', None, None, ids[i]))
+                drop[i] = True
+    valid = np.flatnonzero(ok & ~drop)
+    strs = p['strings']
+    tags = tagger.tag([strs[i] for i in valid], fps=np.asarray(t['fingerprint'])[valid].reshape(-1, 4))
+    is_paper = [False] * len(claimed)
+    names: List[Optional[str]] = [None] * len(claimed)
+    for i, (tagged, name) in zip(valid.tolist(), tags):
+        if tagged:
+            is_paper[i], names[i] = True, name
+    rows = zip(repeat('completed'), ok.tolist(), reasons, is_paper, names, ids)
+    if drop.any():
+        results.extend(r for r, d in zip(rows, drop.tolist()) if not d)
+    else:
+        results.extend(rows)
     return results
+
+
+def process_batches(batches, validator, kwargs, locs, tagger):
+    """process_batch over an iterable of claimed batches, pipelined: batch k+1 is compiled on
+    the host (native compiler threads, GIL released) while batch k runs on the device (its
+    own thread, GIL released in the library), and batch k-1's verdict table and tags are
+    built in between.  Yields each batch's result tuples, in order, identical to
+    process_batch's."""
+    if not (hasattr(validator, 'validate_strings') and not kwargs.get('check_regularity', False)
+            and not kwargs.get('fast_point_only', False)):
+        for claimed in batches:
+            if claimed:
+                yield process_batch(claimed, validator, kwargs, locs, tagger)
+        return
+    from concurrent.futures import ThreadPoolExecutor
+    bv = validator._validator()
+    with ThreadPoolExecutor(max_workers=1) as dev:
+        inflight = None          # (claimed, prepared, future of the device result)
+        for claimed in batches:
+            if not claimed:      # idle (None) or empty: flush the batch in flight
+                if inflight is not None:
+                    c0, p0, f0 = inflight
+                    inflight = None
+                    yield _results(c0, p0, bv.finish(p0, f0.result()), locs, tagger)
+                continue
+            p = bv.prepare_strings([s for _, s in claimed])
+            if inflight is not None:
+                c0, p0, f0 = inflight
+                r0 = f0.result()
+                inflight = (claimed, p, dev.submit(bv.run_prepared, p))
+                yield _results(c0, p0, bv.finish(p0, r0), locs, tagger)
+            else:
+                inflight = (claimed, p, dev.submit(bv.run_prepared, p))
+        if inflight is not None:
+            c0, p0, f0 = inflight
+            yield _results(c0, p0, bv.finish(p0, f0.result()), locs, tagger)

@@ -27,8 +27,12 @@ def stream(name, with_index=False):
 
 FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl', 'ff_d4_s2000.jsonl',
           'ff_d4_exp_quarter.jsonl', 'ff_d4_t600.jsonl')
+# kerr_d4_range: the 243 depth-4 stream candidates whose oracle class changed with the round-3
+# rules (edge_kerr_range.txt): underflow at a reference point or on the whole grid (a pass, no
+# evidence of a constant), a value beyond the fp64 range there, and constants that are constant
+# only on the domain (Delta - Abs(Delta)) -- the reference decides 236 of them
 KERR_REF = ('kerr_d1.jsonl', 'kerr_d2.jsonl', 'kerr_d3_s1000.jsonl', 'kerr_d4_s2000.jsonl',
-            'kerr_d4_accepts.jsonl')
+            'kerr_d4_accepts.jsonl', 'kerr_d4_range.jsonl')
 # The reference's Kerr validator at other constants (gen_reference_verdicts.py --kerr-a-value 0
 # [--kerr-op-a-zero]): a_value = 0 with M and a symbolic (kerr validator.py:36-44: the fast point
 # check substitutes a = 0, the constant test and the symbolic stage keep a symbolic, so u = 1 - x

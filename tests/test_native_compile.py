@@ -141,3 +141,42 @@ def test_native_verdicts_match_reference_and_sympy_path(prob, files):
         if ok != r['ok']:
             bad.append((r['expr'], r['reason']))
     assert not bad, bad[:10]
+
+
+def test_compile_batch_mt_identical_to_single_thread():
+    """pdeval_compile_batch_mt (host threads, chunks claimed dynamically) writes exactly the
+    single-threaded compile: same words, offsets and statuses, at several thread counts."""
+    strings = _stream('force_free_d4_validated.txt.gz')[:20000] + ['rho +', 'sqrt(2)*rho', '']
+    pd_ = P.force_free()
+    ops1, off1, st1 = native.compile_native(pd_.problem_id, strings, threads=1)
+    for t in (2, 3, 8):
+        ops, off, st = native.compile_native(pd_.problem_id, strings, threads=t)
+        assert np.array_equal(st, st1) and np.array_equal(off, off1) and np.array_equal(ops, ops1), t
+
+
+@pytest.mark.parametrize('prob', ['force_free', 'kerr_magnetosphere'])
+def test_format_reasons_equals_reason_for(prob):
+    """pdeval_format_reasons (csrc/pdreasons.cpp) == batch.reason_for for every class, with
+    residuals across the whole double range (printf %.2e/%.3e vs Python's format rounding),
+    non-finite values and the rational flag."""
+    from pdeval.batch import format_reasons
+    pd_ = P.get(prob)
+    rng = np.random.default_rng(7)
+    n = 200000
+    st = rng.integers(0, 9, n).astype(np.uint8)
+    vals = rng.standard_normal(n) * 10.0 ** rng.integers(-320, 308, n)
+    # values that sit on a rounding boundary of 3 / 4 significant digits, and specials
+    vals[:2000] = np.array([1.005, 2.675, 9.995, 1.0049999999999999, 0.125, 6.0650e-5] * 334)[:2000]
+    vals[2000:2010] = [np.inf, -np.inf, np.nan, -np.nan, 0.0, -0.0, 5e-324, 1.7976931348623157e308, 1e-20, 1e-10]
+    n_ref = 1 if prob == 'force_free' else 3
+    res = np.repeat(vals[:, None], n_ref, axis=1) * (1 + np.arange(n_ref))
+    q_ref, q_grid = np.abs(np.roll(vals, 1)), np.abs(np.roll(vals, 2))
+    q_ref[5:10] = [np.nan, np.inf, 0.0, 1e-300, 9.9995e-11]
+    rat = (rng.random(n) < 0.3).astype(np.uint8)
+    notes = [None] * n
+    notes[np.flatnonzero(st == 5)[0]] = 'Float'
+    got = format_reasons(pd_.problem_id, st, res, q_ref, q_grid, rat, notes)
+    want = [reason_for(pd_.problem_id, int(st[i]), res[i], float(q_ref[i]), float(q_grid[i]),
+                       bool(rat[i]), notes[i])[1] for i in range(n)]
+    bad = [(i, got[i], want[i]) for i in range(n) if got[i] != want[i]]
+    assert not bad, bad[:5]
