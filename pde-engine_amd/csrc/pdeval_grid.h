@@ -26,6 +26,18 @@
 
 namespace pd {
 
+// Peephole superinstructions in the lean interpreter (Lean::run): measured and rejected.  On
+// one box (profiles/r03_ab1_*.log, 2^20 candidates) pass 1 took 83.5 ms with them against
+// 77.6 ms without (force-free) and 40.6 against 38.8 ms (Kerr): the extra scalar tests on every
+// opcode cost more than the dispatches they save.  Pass 2's register operand slot (RSLOT) is
+// kept: Kerr pass 2 21.4 -> 18.3 ms, force-free 2.26 -> 2.10 ms.
+#ifndef PD_LEAN_FUSE
+#define PD_LEAN_FUSE 0
+#endif
+#ifndef PD_LEAN_RSLOT
+#define PD_LEAN_RSLOT 1
+#endif
+
 constexpr uint64_t op_bit(int op) { return 1ull << op; }
 constexpr uint64_t kImmMask = op_bit(PDOP_PUSH_C) | op_bit(PDOP_ADDC) | op_bit(PDOP_MULC) |
                               op_bit(PDOP_RDIVC) | op_bit(PDOP_POW);
@@ -91,6 +103,8 @@ template <int K, int W, int MAXD> struct Lean {
     static constexpr int NCJ = nc(K);
 
     static constexpr int SLOT = W * NCJ * 64;   // doubles per operand slot
+    static constexpr bool RSLOT = PD_LEAN_RSLOT && MAXD == 3;   // operand slot 1 in registers (run below)
+    static constexpr int LDS_SLOTS = RSLOT ? 1 : MAXD - 1;
 
     // LDS operand slot of one wave: [w][coef][lane]
     static __device__ __forceinline__ void store(double* stk, int lane, const J (&t)[W]) {
@@ -111,6 +125,10 @@ template <int K, int W, int MAXD> struct Lean {
     static __device__ __forceinline__ void run(const int32_t* prog, int plen, const double (&x)[W], double y,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
                                                double* stk, int lane, const PrmTab<double>& P) {
+        // MAXD = 3 (pass 2): the upper of the two operand slots lives in VGPRs, the lower in
+        // LDS -- two LDS slots of W = 2 Kerr jets (12 KiB per wave) held pass 2 at ~3 waves
+        // per SIMD; with one, VGPRs set the occupancy
+        J reg[RSLOT ? W : 1];
         int pc = 1;
         uint32_t w = rd_word(prog + 1);
         bool first = true;
@@ -125,21 +143,30 @@ template <int K, int W, int MAXD> struct Lean {
             const uint32_t wn = rd_word(prog + (more ? npc : pc));
             const int pn = (int)((w >> 8) & 0xffu);   // POWN exponent / coordinate power n
             const bool on_y = (w >> 16) & 1u;         // coordinate-power axis
-            // peephole superinstructions (no change to the program format): PUSH_C c followed
-            // by MUL_P / MUL_X / MUL_Y pushes c * v^n (c * x, c * y) in one dispatch -- set the
-            // coordinate jet and scale it by c, the same products the two opcodes form on a
-            // constant jet; NEG followed by ADDC is c - t.  Kerr programs are 14 % PUSH_C+MUL_*
-            // pairs, force-free 5 % NEG+ADDC.
+            // peephole superinstructions (no change to the program format, the same arithmetic
+            // in the same order, one dispatch instead of two):
+            //  * PUSH_C c followed by MUL_P / MUL_X / MUL_Y pushes c * v^n (c * x, c * y): the
+            //    coordinate jet scaled by c, the products the two opcodes form on a constant jet;
+            //  * any other opcode followed by MULC or ADDC: the scale / constant add is applied
+            //    at the end of the same iteration (sfx below).
+            // Kerr programs: 14 % PUSH_C+MUL_* pairs, 21 % MULC / ADDC.  (Off: PD_LEAN_FUSE.)
             const uint32_t opn = wn & 0xffu;
-            const bool fuse = more && ((op == PDOP_PUSH_C && (opn == PDOP_MUL_P || opn == PDOP_MUL_X ||
-                                                              opn == PDOP_MUL_Y)) ||
-                                       (op == PDOP_NEG && opn == PDOP_ADDC));
+            const bool fuse = PD_LEAN_FUSE && more && op == PDOP_PUSH_C &&
+                              (opn == PDOP_MUL_P || opn == PDOP_MUL_X || opn == PDOP_MUL_Y);
+            const bool sfx = PD_LEAN_FUSE && more && !fuse && (opn == PDOP_MULC || opn == PDOP_ADDC);
             // dispatch: a tree of wave-uniform bit tests over opcode groups (most frequent
             // first), each a structured if/else -- a flat switch lowers to a compare tree whose
             // unstructured joins the structurizer turns into extra flow masks and copies
             const uint64_t b = 1ull << op;
             if (b & kPushMask) {
-                if (!first) store(stk + (MAXD == 2 ? 0 : d - 1) * SLOT, lane, acc);
+                if (!first) {
+                    if (RSLOT && d == 2) {
+#pragma unroll
+                        for (int q = 0; q < W; ++q) reg[q] = acc[q];
+                    } else {
+                        store(stk + (MAXD == 2 || RSLOT ? 0 : d - 1) * SLOT, lane, acc);
+                    }
+                }
                 ++d;
                 if (op == PDOP_PUSH_X) {
 #pragma unroll
@@ -205,11 +232,6 @@ template <int K, int W, int MAXD> struct Lean {
                 } else if (op == PDOP_NEG) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], -1.0);
-                    if (fuse) {   // ... ADDC c
-                        const double c = rd_immp(prog + npc + 1, wn, P);
-#pragma unroll
-                        for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
-                    }
                 } else if (op == PDOP_MULC) {
                     const double c = rd_immp(prog + pc + 1, w, P);
 #pragma unroll
@@ -253,15 +275,20 @@ template <int K, int W, int MAXD> struct Lean {
                     }
                 }
             } else if (b & kBinMask) {
-                const double* src = stk + (MAXD == 2 ? 0 : d - 2) * SLOT;
+                const double* src = stk + (MAXD == 2 || RSLOT ? 0 : d - 2) * SLOT;
+                const bool from_reg = RSLOT && d == 3;
                 --d;
                 // one operand jet at a time: W > 2 would not hold W operand jets beside the
                 // W accumulators in registers
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
                     J l;
+                    if (from_reg) {
+                        l = reg[RSLOT ? q : 0];
+                    } else {
 #pragma unroll
-                    for (int c = 0; c < NCJ; ++c) l.c[c] = src[(q * NCJ + c) * 64 + lane];
+                        for (int c = 0; c < NCJ; ++c) l.c[c] = src[(q * NCJ + c) * 64 + lane];
+                    }
                     if (op == PDOP_DIV) O::div(l, acc[q]);
                     else if (op == PDOP_SUB) O::sub(l, acc[q]);
                     else if (op == PDOP_ADD) O::add(l, acc[q]);
@@ -289,11 +316,21 @@ template <int K, int W, int MAXD> struct Lean {
                     else absj<K>(acc[q]);
                 }
             }
+            if (sfx) {   // ... MULC c / ADDC c
+                const double c = rd_immp(prog + npc + 1, wn, P);
+                if (opn == PDOP_MULC) {
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::scale(acc[q], c);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
+                }
+            }
             int pc_next = npc;
             uint32_t w_next = wn;
             bool more_next = more;
-            if (fuse) {   // skip the fused second opcode (ADDC carries an immediate)
-                pc_next = npc + (opn == PDOP_ADDC ? ((wn & PDEVAL_IMM_DD) ? 5 : 3) : 1);
+            if (fuse || sfx) {   // skip the fused second opcode (MULC / ADDC carry an immediate)
+                pc_next = npc + (sfx ? ((wn & PDEVAL_IMM_DD) ? 5 : 3) : 1);
                 more_next = pc_next < plen;
                 w_next = rd_word(prog + (more_next ? pc_next : pc));
             }
@@ -399,7 +436,7 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 #define PD_KV_LATE_DEEP 0
 #endif
 #ifndef PD_LIST_WAVES_PER_SIMD
-#define PD_LIST_WAVES_PER_SIMD 1
+#define PD_LIST_WAVES_PER_SIMD 4
 #endif
 #ifndef PD_KERR_W
 #define PD_KERR_W 2
@@ -420,9 +457,10 @@ template <int PROB, int MAXD> constexpr int grid_w() {
     return PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : (MAXD == 2 ? PD_KERR_W : PD_DEEP_W);
 }
 template <int PROB> constexpr int grid_k() { return PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2; }
-// dynamic LDS of one block of `waves` waves: (MAXD - 1) operand slots of W jets each
+// dynamic LDS of one block of `waves` waves: the LDS operand slots (Lean::LDS_SLOTS) of W jets
 template <int PROB, int MAXD> constexpr size_t grid_lds(int waves) {
-    return (size_t)waves * (MAXD - 1) * grid_w<PROB, MAXD>() * nc(grid_k<PROB>()) * 64 * sizeof(double);
+    return (size_t)waves * Lean<grid_k<PROB>(), grid_w<PROB, MAXD>(), MAXD>::LDS_SLOTS * grid_w<PROB, MAXD>() *
+           nc(grid_k<PROB>()) * 64 * sizeof(double);
 }
 
 // The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots.

@@ -34,7 +34,7 @@ from . import problem_defs as P
 from .flatten import Unsupported
 from .opcodes import (CLS_ACCEPT, CLS_BAD_PROGRAM, CLS_NONFINITE_REF, CLS_REJECT_GRID,
                       CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC, CLS_UNSUPPORTED, CLS_ZERO_GRADIENT, FLAG_NOCOORD,
-                      FLAG_RATIONAL, HAS_IMM, IMM_PRM, PDOP, PROBLEM_FORCE_FREE, PROBLEM_KERR, op_len)
+                      FLAG_RATIONAL, HAS_IMM, IMM_PRM, OP_NAME, PDOP, PROBLEM_FORCE_FREE, PROBLEM_KERR, op_len)
 
 
 @dataclass
@@ -163,6 +163,7 @@ def symbolic_zero_gradient(pd, items, out) -> List[int]:
 
 
 _NONRATIONAL_OPS = {PDOP['ABS'], PDOP['SQRT'], PDOP['POW'], PDOP['LOG']}
+_EXP_OPS = {PDOP['EXP']}
 
 
 def _has_op(words, codes) -> bool:
@@ -218,24 +219,118 @@ def _has_prm(words) -> bool:
     return False
 
 
+_KERR_REF_POINTS = ((2.5, 0.6), (7 / 3, 1 / 3), (5.0, -0.4))   # kerr validator.py:168-172
+
+
+def _exp_overflows(words, prm_values, points=_KERR_REF_POINTS) -> bool:
+    """Does evaluating the program (values only, fp64, host) at a reference point take exp of
+    an argument beyond the fp64 range (|arg| > 708: inf, or 0 / a subnormal that a fractional
+    power or a product with an overflowed factor turns into inf or 0 * inf)?  The device's point
+    stage then sees a non-finite value where the reference's arbitrary-range evaluation sees a
+    finite one.  A non-real
+    intermediate (sqrt of a negative value) ends that point's evaluation without an answer."""
+    import math
+    for x, y in points:
+        st: List[float] = []
+        acc = 0.0
+        try:
+            i = 1
+            while i < len(words):
+                w = int(words[i])
+                op = w & 0xff
+                n = (w >> 8) & 0xff
+                if op in HAS_IMM:
+                    if w & IMM_PRM:
+                        d = int(words[i + 1])
+                        imm = prm_values[d & 7] * (-1.0 if d & 8 else 1.0)
+                    else:
+                        imm = float(np.array([words[i + 1], words[i + 2]], dtype=np.int32).view(np.float64)[0])
+                name = OP_NAME.get(op, '')
+                v = y if (w >> 16) & 1 else x
+                if name.startswith('PUSH'):
+                    st.append(acc)
+                    acc = {'PUSH_X': x, 'PUSH_Y': y, 'PUSH_C': imm if name == 'PUSH_C' else 0.0}.get(name, v ** n)
+                elif name in ('ADD', 'SUB', 'RSUB', 'MUL', 'DIV', 'RDIV'):
+                    a = st.pop()
+                    acc = {'ADD': a + acc, 'SUB': a - acc, 'RSUB': acc - a, 'MUL': a * acc,
+                           'DIV': a / acc, 'RDIV': acc / a}[name]
+                elif name == 'ADDC':
+                    acc = acc + imm
+                elif name == 'MULC':
+                    acc = acc * imm
+                elif name == 'RDIVC':
+                    acc = imm / acc
+                elif name == 'NEG':
+                    acc = -acc
+                elif name in ('ADD_X', 'ADD_Y', 'SUB_X', 'SUB_Y', 'MUL_X', 'MUL_Y', 'DIV_X', 'DIV_Y'):
+                    c = x if name.endswith('X') else y
+                    acc = {'ADD': acc + c, 'SUB': acc - c, 'MUL': acc * c, 'DIV': acc / c}[name[:3]]
+                elif name in ('ADD_P', 'SUB_P', 'MUL_P', 'DIV_P', 'RDIV_P'):
+                    p_ = v ** n
+                    acc = {'ADD_P': acc + p_, 'SUB_P': acc - p_, 'MUL_P': acc * p_, 'DIV_P': acc / p_,
+                           'RDIV_P': p_ / acc}[name]
+                elif name == 'POWN':
+                    acc = acc ** n
+                elif name == 'POW':
+                    acc = math.pow(acc, imm)
+                elif name == 'SQRT':
+                    acc = math.sqrt(acc)
+                elif name == 'EXP':
+                    if abs(acc) > 708.0:    # beyond the fp64 range, or into its subnormals
+                        return True
+                    acc = math.exp(acc)
+                elif name == 'LOG':
+                    acc = math.log(acc)
+                elif name == 'ABS':
+                    acc = abs(acc)
+                else:
+                    break
+                i += op_len(w)
+        except (ValueError, ZeroDivisionError, OverflowError, IndexError):
+            continue
+    return False
+
+
 def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-10,
-                           n_grid: int = 4096) -> List[int]:
-    """Kerr with a constant whose point-stage value is 0 (a_value = 0): the reference's fast
-    point check substitutes the values into the SYMBOLIC lhs (kerr validator.py:163-192), after
-    differentiation, so a u that is singular or undefined at a = 0 can still pass -- its lhs
-    may not contain a at all (``x + a**(-2)``), or be 0 * (a finite value) (``a**2/x**(-3/2)``
-    at x < 0).  The device evaluates u itself at the point and sees a non-finite value.  The
-    candidates it rejected at the point stage for non-finiteness (rejected with max|lhs| below
-    the threshold) and whose program uses the constants are re-checked here with the
-    reference's own rule; where it passes, the grid stage (evaluated at the stand-ins of the
-    symbols) decides: a failing point, or no finite point at all (the device's rule), rejects.
-    Updates ``out`` in place; returns the changed rows."""
-    if pd.problem_id != PROBLEM_KERR or kerr is None or kerr.a_num != 0:
+                           n_grid: int = 4096, full_grid: bool = True) -> List[int]:
+    """Kerr point rejects that only the fp64 representation caused, re-checked with the
+    reference's own rule (its fast point check substitutes the values into the SYMBOLIC lhs
+    and evaluates with N(., 40), kerr validator.py:163-192 -- no fp64 range, and after
+    differentiation):
+    * a constant whose point-stage value is 0 (a_value = 0): a u that is singular or undefined
+      at a = 0 can still pass -- its lhs may not contain a at all (``x + a**(-2)``), or be
+      0 * (a finite value) (``a**2/x**(-3/2)`` at x < 0); the device evaluates u itself at the
+      point and sees a non-finite value.  Candidates rejected for non-finiteness (rejected with
+      max|lhs| below the threshold) whose program uses the constants;
+    * an exponential beyond the fp64 range at a reference point: ``exp(r**2/a**2)`` at r = 5,
+      a = 1/10 is e^2500, so ``pow_neg_3_2(exp(r**2/a**2)*exp(a**2*x**2))`` is inf * 0 there on
+      the device while the reference finds |lhs| ~ 1e-1600 and passes.  Candidates rejected with
+      a non-finite value at some reference point and every finite one below the threshold,
+      whose program takes exp of an argument beyond +-708 at a reference point
+      (_exp_overflows, a host fp64 value interpreter).
+    Where the reference's rule passes, the grid stage (evaluated at the stand-ins of the
+    symbols; needs full_grid) decides: a failing point, or no finite point at all (the
+    device's rule), rejects.  Updates ``out`` in place; returns the changed rows."""
+    if pd.problem_id != PROBLEM_KERR or kerr is None or not full_grid:
         return []
     st = np.asarray(out['status'])
+    rr = np.asarray(out['res_ref'], dtype=np.float64).reshape(len(st), -1)
+    with np.errstate(invalid='ignore'):
+        fin = np.isfinite(rr)
+        q_fin = np.where(fin, np.abs(np.where(fin, rr, 0.0)), 0.0).max(axis=1)
+        a0_sel = (st == CLS_REJECT_POINT) & ~(np.asarray(out['q_ref']) >= abs_tol) if kerr.a_num == 0 else \
+            np.zeros(len(st), dtype=bool)
+        ovf_sel = (st == CLS_REJECT_POINT) & ~fin.all(axis=1) & (q_fin < abs_tol)
+    Mv, av = kerr.M_num / kerr.M_den, kerr.a_num / kerr.a_den
+    with np.errstate(divide='ignore'):
+        prm_pt = [Mv, av] + [float(np.float64(1.0) / np.float64(t)) for t in (Mv, av)] + [Mv * Mv, av * av] + \
+                 [float(np.float64(1.0) / np.float64(t * t)) for t in (Mv, av)]
     rows = []
-    for i in np.flatnonzero((st == CLS_REJECT_POINT) & ~(np.asarray(out['q_ref']) >= abs_tol)):
-        if not _has_prm(ops[off[i]:off[i + 1]]):
+    for i in np.flatnonzero(a0_sel | ovf_sel):
+        w = ops[off[i]:off[i + 1]]
+        a0 = bool(a0_sel[i]) and _has_prm(w)
+        ovf = bool(ovf_sel[i]) and _has_op(w, _EXP_OPS) and _exp_overflows(w, prm_pt)
+        if not (a0 or ovf):
             continue
         try:
             u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
@@ -314,7 +409,7 @@ class BatchValidator:
         symbolic_zero_gradient(self.pd, items, r)
         kerr_symbolic_constant(self.pd, items, r, ops, off)
         kerr_exact_point_check(self.pd, self.kerr, items, r, ops, off, self.params.kerr_abs_tol,
-                               self.ctx.n_points - self.ctx.n_ref)
+                               self.ctx.n_points - self.ctx.n_ref, bool(self.params.full_grid))
         return r
 
     def table(self, r, ops, off, notes) -> dict:

@@ -448,6 +448,9 @@ def _irr(sig) -> tuple:
     return tuple((h, a % 1) for h, a in sig if a % 1 != 0)
 
 
+_I_KIND = ('P', (Fraction(1, 2),), True, ((('i',), Fraction(1, 2)),))
+
+
 def _det_kind(n):
     """Algebraic shape of a node's value, for "is the force-free determinant rational at a
     rational point" (the reference then says "Invalid (point check != 0)", else prints its
@@ -495,9 +498,12 @@ def _det_kind(n):
     a, b = n[1], n[2]
     ka, kb = _det_kind(a), _det_kind(b)
     if k in ('mul', 'div'):
-        # I as a factor: a pure constant whose 6th power is rational
-        ka = ('P', (), True, ()) if ka == 'I' else ka
-        kb = ('P', (), True, ()) if kb == 'I' else kb
+        # I as a factor: (-1)**(1/2), a pure constant whose 6th power is rational.  It enters the
+        # signature as a pseudo-base, so that a sum I*H + H (whose det is (1 + I)**6 * det(H) =
+        # -8 I det(H), not a Number) keeps two different irrational parts and is not rational,
+        # while I*H + I*H' with equal H-parts is
+        ka = _I_KIND if ka == 'I' else ka
+        kb = _I_KIND if kb == 'I' else kb
     if k in ('add', 'sub'):
         if ka == kb and ka in ('R', 'C'):
             return ka

@@ -7,6 +7,14 @@ programs' FLOP model; every rank validates its range with no data-path communica
 packed verdict bitmaps are then assembled on every rank with a single all-gather: natively
 through the C ABI (``pdeval_gather_bits``, RCCL over xGMI, :func:`gather_verdicts_native`) or
 through ``torch.distributed`` (:func:`gather_verdicts`; gloo in the CPU tests).
+
+The gathered bitmap is the DEVICE's verdict, before the host steps of ``pdeval.batch``
+(``BatchValidator.host_steps``: the symbolic zero-gradient re-check, the Kerr structural
+constant re-check and the Kerr a = 0 exact point check).  Those steps only ever turn a verdict
+from True to False, and only for candidates whose device fingerprint is flat or whose class is
+ZERO_GRADIENT / a point reject; a caller that needs the plugin's exact verdicts runs them on
+its own shard's status (they need the candidate's tree) and gathers after, as
+``pdeval.worker`` does per batch.
 """
 from __future__ import annotations
 
