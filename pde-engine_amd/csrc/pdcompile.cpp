@@ -85,6 +85,55 @@ Rat rpow_int(Rat b, int64_t n) {
     for (int64_t i = 0; i < n; ++i) r = rmul(r, b);
     return r;
 }
+// ---- integer helpers of SymPy's numeric powers (Integer._eval_power)
+const int64_t kRadMax = (int64_t)1 << 30;   // bases factored exactly by trial division to 2^15
+// exact integer n-th root of x >= 0, or -1
+int64_t nthroot_exact(int64_t x, int64_t n) {
+    if (x < 2) return x;
+    int64_t r = (int64_t)std::llround(std::pow((double)x, 1.0 / (double)n));
+    for (int64_t c = std::max<int64_t>(1, r - 1); c <= r + 1; ++c) {
+        __int128 v = 1;
+        for (int64_t k = 0; k < n && v <= x; ++k) v *= c;
+        if (v == x) return c;
+    }
+    return -1;
+}
+// sympy.ntheory.perfect_power(n) (big=True): (b, e) with the largest e > 1, b**e == n
+bool perfect_power(int64_t n, int64_t* b, int64_t* e) {
+    for (int64_t k = 62; k >= 2; --k) {
+        if (((int64_t)1 << std::min<int64_t>(k, 62)) > n && k > 1) continue;   // 2**k > n
+        const int64_t r = nthroot_exact(n, k);
+        if (r >= 2) { *b = r; *e = k; return true; }
+    }
+    return false;
+}
+// factorint(n) for n <= 2^30: (prime, exponent) in increasing prime order
+std::vector<std::pair<int64_t, int64_t>> factorint(int64_t n) {
+    std::vector<std::pair<int64_t, int64_t>> f;
+    for (int64_t p = 2; p * p <= n; ++p) {
+        if (n % p) continue;
+        int64_t k = 0;
+        while (n % p == 0) { n /= p; ++k; }
+        f.push_back({p, k});
+    }
+    if (n > 1) f.push_back({n, 1});
+    return f;
+}
+int64_t igcd(int64_t a, int64_t b) {
+    a = a < 0 ? -a : a;
+    b = b < 0 ? -b : b;
+    while (b) { const int64_t t = a % b; a = b; b = t; }
+    return a;
+}
+int64_t ipow_checked(int64_t b, int64_t e) {
+    __int128 v = 1;
+    for (int64_t k = 0; k < e; ++k) {
+        v *= b;
+        if (v > kRatMax) throw Decline{};
+    }
+    return (int64_t)v;
+}
+
 std::string rstr(Rat a) {
     std::string s = std::to_string(a.p);
     if (a.q != 1) s += "/" + std::to_string(a.q);
@@ -92,7 +141,7 @@ std::string rstr(Rat a) {
 }
 
 // ------------------------------------------------------------------ the expression DAG
-enum Kind : uint8_t { NUM, SYM, ADD, MUL, POW, EXP, ABS };
+enum Kind : uint8_t { NUM, SYM, ADD, MUL, POW, EXP, ABS, IMAG };   // IMAG: SymPy's I
 
 struct Node {
     Kind k;
@@ -123,7 +172,7 @@ struct Ctx {
     // a deque: references to nodes stay valid while evaluation appends new ones
     std::deque<Node> nodes;
     std::unordered_map<std::string, int> intern;
-    int ZERO = -1, ONE = -1, NEG1 = -1;
+    int ZERO = -1, ONE = -1, NEG1 = -1, IU = -1;
 
     void reset(const SymInfo* s, int n) {
         syms = s;
@@ -133,6 +182,7 @@ struct Ctx {
         ZERO = num(Rat{0, 1});
         ONE = num(Rat{1, 1});
         NEG1 = num(Rat{-1, 1});
+        IU = make(Node{IMAG, {}, -1, {}, "I"});
     }
     const Node& N(int i) const { return nodes[i]; }
     int make(Node&& nd) {
@@ -187,6 +237,7 @@ struct Ctx {
         const Node& n = nodes[i];
         switch (n.k) {
             case NUM: case SYM: case ABS: return YES;
+            case IMAG: return UNK;   // (is_extended_real is False; only YES is acted on)
             case ADD: case MUL: {
                 for (int c : n.a) if (real(c, zoo_ok) != YES) return UNK;
                 return YES;
@@ -219,6 +270,8 @@ struct Ctx {
                 return u;
             case ABS:
                 return Sign{UNK, YES, NO, UNK};
+            case IMAG:
+                return u;
             case EXP:
                 if (real(n.a[0]) == YES) return Sign{YES, YES, NO, NO};
                 return u;
@@ -369,19 +422,24 @@ struct Ctx {
         }
         Rat coeff{1, 1};
         std::vector<BE> pw;
+        std::vector<int> seq(in.begin(), in.end());
         for (const BE& x : pre) {
             if (is_num(x.base)) {   // Pow(Number, Integer) folds into the coefficient
-                if (!rint(x.c)) throw Decline{};
-                coeff = rmul(coeff, rpow_int(rv(x.base), x.c.p));
+                if (rint(x.c)) coeff = rmul(coeff, rpow_int(rv(x.base), x.c.p));
+                else seq.push_back(raw_pow(x.base, num(x.c)));   // Pow(Number, e, evaluate=False)
             } else {
                 pw.push_back(x);
             }
         }
-        std::vector<int> seq(in.begin(), in.end());
+        // numeric bases with rational powers (pnum_rat), base -> exponents, insertion order;
+        // neg1e, the exponent of -1 collected from I and from negative numeric bases
+        std::vector<std::pair<Rat, std::vector<Rat>>> pnum_rat;
+        Rat neg1e{0, 1};
         for (size_t i = 0; i < seq.size(); ++i) {
             const int o = seq[i];
             const Node& n = nodes[o];
             if (n.k == NUM) { coeff = rmul(coeff, n.r); continue; }
+            if (n.k == IMAG) { neg1e = radd(neg1e, Rat{1, 2}); continue; }
             if (n.k == MUL) { for (int c : n.a) seq.push_back(c); continue; }
             if (n.k == EXP) {
                 auto cm = coeff_mul(n.a[0]);
@@ -390,7 +448,19 @@ struct Ctx {
             }
             if (n.k == POW) {
                 if (!is_num(n.a[1])) throw Decline{};
-                if (is_num(n.a[0])) throw Decline{};   // numeric base with a rational power
+                if (is_num(n.a[0])) {
+                    const Rat b = rv(n.a[0]), ex = rv(n.a[1]);
+                    if (rint(ex)) { coeff = rmul(coeff, rpow_int(b, ex.p)); continue; }
+                    if (ex.p < 0) { seq.push_back(pow_(n.a[0], n.a[1])); continue; }   // evaluated
+                    Rat bb = b;
+                    if (b.p < 0) { neg1e = radd(neg1e, ex); bb = rneg(b); }
+                    if (req(bb, Rat{1, 1})) continue;
+                    bool found = false;
+                    for (auto& pr : pnum_rat)
+                        if (req(pr.first, bb)) { pr.second.push_back(ex); found = true; break; }
+                    if (!found) pnum_rat.push_back({bb, {ex}});
+                    continue;
+                }
                 pw.push_back(BE{n.a[0], rv(n.a[1]), ONE});
                 continue;
             }
@@ -444,6 +514,16 @@ struct Ctx {
             const Node& n = nodes[p];
             if (n.k == NUM) coeff = rmul(coeff, n.r);
             else fac.push_back(p);   // a product from Pow(b, e) stays one nested factor
+        }
+        if (!pnum_rat.empty()) numeric_powers(pnum_rat, coeff, fac);
+        if (neg1e.p != 0) {
+            // treat I as (-1)**(1/2): an odd integer part of the total exponent flips the
+            // coefficient, a half leaves I; other fractions ((-1)**(1/4) ...) are not restated
+            const int64_t nn = (neg1e.p - (((neg1e.p % neg1e.q) + neg1e.q) % neg1e.q)) / neg1e.q;   // floor
+            const int64_t pp = neg1e.p - nn * neg1e.q;
+            if (nn % 2) coeff = rneg(coeff);
+            if (neg1e.q == 2) fac.push_back(IU);
+            else if (pp) throw Decline{};
         }
         if (coeff.p == 0) return ZERO;
         if (fac.empty()) return num(coeff);
@@ -580,7 +660,13 @@ struct Ctx {
             if (rint(ex)) return num(rpow_int(bn.r, ex.p));
             if (req(bn.r, Rat{1, 1})) return ONE;
             if (bn.r.p == 0 && ex.p > 0) return ZERO;
-            throw Decline{};     // irrational numeric power (sqrt(2) ...)
+            if (bn.r.p > 0) return num_pow(bn.r, ex);
+            return neg_num_pow(bn.r, ex);
+        }
+        if (bn.k == IMAG) {      // ImaginaryUnit._eval_power: I**n, integer n
+            if (!rint(ex)) throw Decline{};
+            const int64_t k = ((ex.p % 4) + 4) % 4;
+            return k == 0 ? ONE : (k == 1 ? IU : (k == 2 ? NEG1 : mul({NEG1, IU})));
         }
         switch (bn.k) {
             case EXP: {
@@ -636,6 +722,177 @@ struct Ctx {
                 return raw_pow(b, e);
         }
     }
+    // Pow(b, e) for a negative Rational b and a non-integer e with denominator 2
+    // (Integer._eval_power / Rational._eval_power with NegativeOne._eval_power: (-1)**(p/2) =
+    // I**p): (-b)**e * I**p, Python's product; other denominators leave (-1)**e unevaluated,
+    // which is not restated
+    int neg_num_pow(Rat b, Rat e) {
+        if (e.q != 2) throw Decline{};
+        const Rat pb = rneg(b);
+        if (b.q == 1 && req(e, Rat{1, 2})) return mul({IU, pow_(num(pb), num(e))});   // I*sqrt(-b)
+        if (b.q != 1) throw Decline{};   // (Rational bases: not met in these streams)
+        const int ip = pow_(IU, num(Rat{e.p, 1}));
+        if (e.p < 0) {
+            // S.NegativeOne**expt * Rational(1, -b)**ne
+            return mul({ip, pow_(num(Rat{1, pb.p}), num(rneg(e)))});
+        }
+        // the positive part evaluates first (perfect root or extracted factors), then * (-1)**e
+        const int r = pow_(num(pb), num(e));
+        if (nodes[r].k == POW && nodes[r].a[0] != -1 && is_num(nodes[r].a[0]) && req(rv(nodes[r].a[0]), pb) &&
+            req(rv(nodes[r].a[1]), e))
+            throw Decline{};   // result None: SymPy keeps Pow(b, e) with the negative base
+        return mul({r, ip});
+    }
+
+    // ---- numeric radicals: Pow(b, e) for a Rational b > 0 and a non-integer Rational e
+    // (Integer._eval_power / Rational._eval_power, sympy/core/numbers.py): perfect roots and
+    // extracted factors evaluate, the rest stays an unevaluated Pow(b', e') with b' an integer
+    int num_pow(Rat b, Rat e) {
+        if (req(b, Rat{1, 1})) return ONE;
+        if (b.p > kRadMax || b.q > kRadMax || e.q > 64 || e.p > 64 * e.q || e.p < -64 * e.q) throw Decline{};
+        if (e.p < 0) return num_pow(Rat{b.q, b.p}, rneg(e));   // (p/q)**-e = (q/p)**e
+        if (b.q == 1) return int_pow(b.p, e);
+        // Rational._eval_power: p**e * q**(k - e) / q**k with k = floor(e) + 1
+        const int64_t p = b.p, q = b.q;
+        int64_t ip = e.p / e.q;
+        Rat rf;
+        int64_t qk;
+        if (ip) {
+            ip += 1;
+            rf = mkrat((__int128)ip * e.q - e.p, e.q);
+            qk = ipow_checked(q, ip);
+        } else {
+            rf = mkrat((__int128)e.q - e.p, e.q);
+            qk = q;
+        }
+        const int fq = pow_(num(Rat{q, 1}), num(rf));
+        const int ab = p != 1 ? mul({pow_(num(Rat{p, 1}), num(e)), fq}) : fq;
+        return mul({ab, num(Rat{1, qk})});
+    }
+    int int_pow(int64_t b, Rat e) {
+        // a perfect root: sqrt(4) -> 2
+        const int64_t x = nthroot_exact(b, e.q);
+        if (x >= 0) return num(Rat{ipow_checked(x, e.p), 1});
+        std::vector<std::pair<int64_t, int64_t>> dict;
+        int64_t pb, pe;
+        if (perfect_power(b, &pb, &pe)) dict.push_back({pb, pe});
+        else dict = factorint(b);
+        int64_t out_int = 1, sqr_gcd = 0;
+        int out_rad = -1;   // product of the extracted radicals (None: 1)
+        std::vector<std::pair<int64_t, int64_t>> sqr;
+        for (const auto& pr : dict) {
+            const int64_t ex = pr.second * e.p;
+            const int64_t de = ex / e.q, dm = ex % e.q;
+            if (de > 0) out_int = (int64_t)std::min<__int128>((__int128)out_int * ipow_checked(pr.first, de), kRatMax + 1);
+            if (out_int > kRatMax) throw Decline{};
+            if (dm > 0) {
+                const int64_t g = igcd(dm, e.q);
+                if (g != 1) {
+                    const int r = pow_(num(Rat{pr.first, 1}), num(Rat{dm / g, e.q / g}));
+                    out_rad = out_rad < 0 ? r : mul({out_rad, r});
+                } else {
+                    sqr.push_back({pr.first, dm});
+                }
+            }
+        }
+        for (const auto& pr : sqr) {
+            sqr_gcd = sqr_gcd == 0 ? pr.second : igcd(sqr_gcd, pr.second);
+            if (sqr_gcd == 1) break;
+        }
+        int64_t sqr_int = 1;
+        for (const auto& pr : sqr) sqr_int = ipow_checked(sqr_int, 1) * ipow_checked(pr.first, pr.second / sqr_gcd);
+        if (sqr_int == b && out_int == 1 && out_rad < 0) return raw_pow(num(Rat{b, 1}), num(e));
+        // out_int * out_rad * Pow(sqr_int, sqr_gcd / e.q), Python's left-to-right products
+        int acc = num(Rat{out_int, 1});
+        if (out_rad >= 0) acc = mul({acc, out_rad});
+        const int last = sqr_gcd == 0 ? ONE : pow_(num(Rat{sqr_int, 1}), num(mkrat(sqr_gcd, e.q)));
+        return mul({acc, last});
+    }
+
+    // Mul.flatten's numeric powers (part 2 of sympy/core/mul.py): pnum_rat, base -> exponents
+    // in insertion order; returns the factors to add to the product, folds numbers into coeff
+    void numeric_powers(const std::vector<std::pair<Rat, std::vector<Rat>>>& pnum_rat, Rat& coeff,
+                        std::vector<int>& fac) {
+        // comb_e: summed exponent -> bases
+        std::vector<std::pair<Rat, std::vector<Rat>>> comb;
+        for (const auto& be : pnum_rat) {
+            Rat es{0, 1};
+            for (Rat r : be.second) es = radd(es, r);
+            bool found = false;
+            for (auto& c : comb)
+                if (req(c.first, es)) { c.second.push_back(be.first); found = true; break; }
+            if (!found) comb.push_back({es, {be.first}});
+        }
+        std::vector<std::pair<Rat, Rat>> num_rat;   // (base, exponent)
+        for (auto& c : comb) {
+            Rat bb{1, 1};
+            for (Rat r : c.second) bb = rmul(bb, r);
+            Rat e = c.first;
+            if (e.q == 1) { coeff = rmul(coeff, rpow_int(bb, e.p)); continue; }
+            if (e.p > e.q) {
+                coeff = rmul(coeff, rpow_int(bb, e.p / e.q));
+                e = Rat{e.p % e.q, e.q};
+            }
+            num_rat.push_back({bb, e});
+        }
+        // gcd extraction: 2**(1/3)*6**(1/4) -> 2**(1/3+1/4) * 3**(1/4)
+        std::vector<std::pair<Rat, std::vector<Rat>>> pnew;   // exponent -> bases
+        auto rgcd = [](Rat a, Rat b) {   // Rational.gcd: gcd of numerators / lcm of denominators
+            const int64_t g = igcd(a.p, b.p), l = a.q / igcd(a.q, b.q) * b.q;
+            return mkrat(g, l);
+        };
+        for (size_t i = 0; i < num_rat.size(); ++i) {
+            Rat bi = num_rat[i].first;
+            const Rat ei = num_rat[i].second;
+            if (req(bi, Rat{1, 1})) continue;
+            std::vector<std::pair<Rat, Rat>> grow;
+            for (size_t j = i + 1; j < num_rat.size(); ++j) {
+                const Rat bj = num_rat[j].first, ej = num_rat[j].second;
+                const Rat g = rgcd(bi, bj);
+                if (!req(g, Rat{1, 1})) {
+                    Rat e = radd(ei, ej);
+                    if (e.q == 1) {
+                        coeff = rmul(coeff, rpow_int(g, e.p));
+                    } else {
+                        if (e.p > e.q) {
+                            coeff = rmul(coeff, rpow_int(g, e.p / e.q));
+                            e = Rat{e.p % e.q, e.q};
+                        }
+                        grow.push_back({g, e});
+                    }
+                    num_rat[j].first = rmul(bj, Rat{g.q, g.p});
+                    bi = rmul(bi, Rat{g.q, g.p});
+                    if (req(bi, Rat{1, 1})) break;
+                }
+            }
+            if (!req(bi, Rat{1, 1})) {
+                const int obj = pow_(num(bi), num(ei));
+                std::vector<int> parts;
+                if (nodes[obj].k == MUL) parts = nodes[obj].a;
+                else parts.push_back(obj);
+                for (int f : parts) {
+                    const Node& fn = nodes[f];
+                    if (fn.k == NUM) { coeff = rmul(coeff, fn.r); continue; }
+                    if (fn.k != POW || !is_num(fn.a[0]) || !is_num(fn.a[1])) throw Decline{};
+                    const Rat fe = rv(fn.a[1]);
+                    bool found = false;
+                    for (auto& pn : pnew)
+                        if (req(pn.first, fe)) { pn.second.push_back(rv(fn.a[0])); found = true; break; }
+                    if (!found) pnew.push_back({fe, {rv(fn.a[0])}});
+                }
+            }
+            for (const auto& gr : grow) num_rat.push_back(gr);
+        }
+        for (const auto& pn : pnew) {
+            Rat bb{1, 1};
+            for (Rat r : pn.second) bb = rmul(bb, r);
+            const int p = pow_(num(bb), num(pn.first));
+            if (nodes[p].k == NUM) { coeff = rmul(coeff, nodes[p].r); continue; }
+            if (nodes[p].k != POW) throw Decline{};   // (a product here: not restated)
+            fac.push_back(p);
+        }
+    }
+
     // Mul._eval_power + Pow._eval_expand_power_base(force=False)
     int pow_mul(int b, int e) {
         const Rat ex = rv(e);
@@ -668,8 +925,35 @@ struct Ctx {
         } else {
             other.insert(other.end(), negs.begin(), negs.end());
         }
-        for (int c : nonneg_)
-            if (is_num(c)) throw Decline{};   // numeric factor under a rational power
+        // Pow._eval_expand_power_base: the numeric radicals among the nonnegative factors
+        // (npow: Pow with a number base) are raised WITH evaluation first, rv = Mul(*[Pow(b, e)
+        // for b in npow]); then rv *= Mul(*[Pow(c, e, evaluate=False) for c in the rest]) and
+        // rv *= Pow(Mul(*other), e, evaluate=False)
+        {
+            std::vector<int> npow, rest;
+            for (int c : nonneg_) {
+                const Node& cn = nodes[c];
+                if (cn.k == POW && is_num(cn.a[0]) && is_num(cn.a[1])) npow.push_back(c);
+                else rest.push_back(c);
+            }
+            if (!npow.empty()) {
+                std::vector<int> ps;
+                for (int c : npow) ps.push_back(pow_(c, e));
+                int rv = ps.size() == 1 ? ps[0] : mul(ps);
+                if (rest.size() == 1) {
+                    rv = mul({rv}, {BE{rest[0], ex, ONE}});
+                } else if (!rest.empty()) {
+                    std::vector<BE> pr;
+                    for (int c : rest) pr.push_back(BE{c, ex, ONE});
+                    rv = mul({rv, mul({}, pr)});
+                }
+                if (!other.empty()) {
+                    const int ob = other.size() == 1 ? other[0] : mul(other);
+                    rv = mul({rv}, {BE{ob, ex, ONE}});
+                }
+                return rv;
+            }
+        }
         // rv = Mul(*[Pow(c, e, evaluate=False) for c in nonneg]); rv *= Pow(Mul(*other), e,
         // evaluate=False)  (a one-factor Mul of an unevaluated Pow is that Pow itself)
         std::vector<BE> pre;
@@ -798,7 +1082,7 @@ struct Parser {
 
 // ------------------------------------------------------------------ lowering (flatten.py)
 // IR nodes as in flatten.py: x y c (neg sqrt exp log abs) pown pow (add sub mul div)
-enum IK : uint8_t { IX, IY, IC, INEG, ISQRT, IEXP, IABS, IPOWN, IPOW, IADD, ISUB, IMUL, IDIV };
+enum IK : uint8_t { IX, IY, IC, INEG, ISQRT, IEXP, IABS, IPOWN, IPOW, IADD, ISUB, IMUL, IDIV, II };   // II: I
 struct IR {
     IK k;
     double c = 0.0;   // IC value / IPOW exponent
@@ -837,7 +1121,7 @@ struct Lower {
     int need(int i) const {
         const IR& x = ir[i];
         switch (x.k) {
-            case IX: case IY: case IC: return 1;
+            case IX: case IY: case IC: case II: return 1;
             case INEG: case ISQRT: case IEXP: case IABS: case IPOWN: case IPOW: return need(x.a);
             default: break;
         }
@@ -878,6 +1162,7 @@ struct Lower {
                 if (nd.a[0] == C.ONE) { IR x{IC}; x.c = kE; x.lo = kELo; x.irr = true; return mk(x); }
                 return un(IEXP, node(nd.a[0]));
             case ABS: return un(IABS, node(nd.a[0]));
+            case IMAG: return mk(IR{II});   // flatten.py ('i',): PUSH_I, header COMPLEX
         }
         throw Decline{};
     }
@@ -981,7 +1266,7 @@ struct Lower {
 
     // ---- det_rational (flatten.py _det_kind / det_rational)
     struct Kd {
-        int t;                    // 0 = None, 1 = 'R', 2 = 'C', 3 = ('P', exps, pure, sig)
+        int t;                    // 0 = None, 1 = 'R', 2 = 'C', 3 = ('P', exps, pure, sig), 4 = 'I'
         std::vector<Rat> ex;
         bool pure = false;
         // sig: prod h**a, exponents summed per base (flatten.py _sig); bases are IR subtrees
@@ -1038,11 +1323,14 @@ struct Lower {
         switch (x.k) {
             case IX: case IY: return Kd{1, {}, false};
             case IC: return Kd{x.irr ? 2 : 1, {}, false};
-            case INEG: case IABS: return kind(x.a);
+            case II: return Kd{4, {}, false};   // a factor I scales det by I**6 = -1
+            case INEG: return kind(x.a);
+            case IABS: { Kd k = kind(x.a); return k.t == 4 ? Kd{1, {}, false} : k; }
             case IEXP: { Kd k = kind(x.a); return k.t == 2 ? Kd{2, {}, false} : Kd{0, {}, false}; }
             case ISQRT: case IPOWN: case IPOW: {
                 const Rat e = x.k == ISQRT ? Rat{1, 2} : (x.k == IPOWN ? Rat{x.n, 1} : x.alpha);
                 Kd k = kind(x.a);
+                if (k.t == 4) return rint(e) ? Kd{(e.p % 2) ? 4 : 1, {}, false} : Kd{0, {}, false};
                 if (k.t == 2) return Kd{2, {}, false};
                 if (k.t == 1) {
                     if (rint(e)) return Kd{1, {}, false};
@@ -1062,6 +1350,12 @@ struct Lower {
         }
         const int a = x.a, b = x.b;
         Kd ka = kind(a), kb = kind(b);
+        if (x.k == IMUL || x.k == IDIV) {
+            // I as a factor: (-1)**(1/2), a pure constant with I as a pseudo-base of the
+            // signature (flatten.py _I_KIND): I*H + H keeps two irrational parts
+            if (ka.t == 4) ka = Kd{3, {Rat{1, 2}}, true, {{a, Rat{1, 2}}}};
+            if (kb.t == 4) kb = Kd{3, {Rat{1, 2}}, true, {{b, Rat{1, 2}}}};
+        }
         if (x.k == IADD || x.k == ISUB) {
             if (ka.t == kb.t && (ka.t == 1 || ka.t == 2)) return Kd{ka.t, {}, false};
             if (ka.t == 3 && kb.t == 3 && same_irr(ka, kb)) {   // r1*H + r2*H = (r1 + r2)*H
@@ -1099,7 +1393,7 @@ struct Lower {
             break;
         }
         Kd k = kind(n);
-        if (k.t == 1 || k.t == 2) return true;
+        if (k.t == 1 || k.t == 2 || k.t == 4) return true;
         if (k.t != 3) return false;
         for (Rat r : k.ex) if (!rint(rmul(r, Rat{6, 1}))) return false;
         return true;
@@ -1114,7 +1408,8 @@ struct Emit {
     explicit Emit(const Lower& l) : L(l) {}
     void op(int code, int arg = 0) {
         w.push_back(code | (arg << 8));
-        if (code == PDOP_PUSH_X || code == PDOP_PUSH_Y || code == PDOP_PUSH_C || code == PDOP_PUSH_P) {
+        if (code == PDOP_PUSH_X || code == PDOP_PUSH_Y || code == PDOP_PUSH_C || code == PDOP_PUSH_P ||
+            code == PDOP_PUSH_I) {
             ++d;
             dmax = std::max(dmax, d);
         } else if (code == PDOP_ADD || code == PDOP_SUB || code == PDOP_RSUB || code == PDOP_MUL ||
@@ -1186,6 +1481,7 @@ struct Emit {
         const IR& x = L.ir[i];
         if (x.k == IX || x.k == IY || x.k == IC || L.is_pvar(i)) { leaf(i); return; }
         switch (x.k) {
+            case II: op(PDOP_PUSH_I); return;
             case INEG: emit(x.a); op(PDOP_NEG); return;
             case ISQRT: emit(x.a); op(PDOP_SQRT); return;
             case IEXP: emit(x.a); op(PDOP_EXP); return;
@@ -1226,7 +1522,7 @@ int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t le
         E.emit(ir);
         if (E.d != 1) return 2;
         if (E.dmax > PDEVAL_MAX_STACK) throw Decline{};   // the SymPy path reports it
-        bool xs = false, ys = false, ab = false;
+        bool xs = false, ys = false, ab = false, im = false;
         for (size_t k = 0; k < E.w.size();) {
             const int o = E.w[k] & 0xff;
             const uint32_t wd = (uint32_t)E.w[k];
@@ -1234,6 +1530,7 @@ int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t le
             if (o == PDOP_PUSH_Y || o == PDOP_ADD_Y || o == PDOP_SUB_Y || o == PDOP_MUL_Y || o == PDOP_DIV_Y) ys = true;
             if (is_p_op(o)) { if ((wd >> 16) & 1) ys = true; else xs = true; }
             if (o == PDOP_ABS) ab = true;
+            if (o == PDOP_PUSH_I) im = true;
             const bool imm = o == PDOP_PUSH_C || o == PDOP_ADDC || o == PDOP_MULC || o == PDOP_RDIVC || o == PDOP_POW;
             k += imm ? ((wd & PDEVAL_IMM_DD) ? 5 : 3) : 1;
         }
@@ -1241,6 +1538,7 @@ int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t le
         if (!(xs || ys)) hdr |= PDEVAL_FLAG_NOCOORD;
         if (L.det_rational(ir)) hdr |= PDEVAL_FLAG_RATIONAL;
         if (xs && ys && ab) hdr |= PDEVAL_FLAG_NONSMOOTH2D;
+        if (im) hdr |= PDEVAL_FLAG_COMPLEX;
         // SymPy keeps exp(g)**(p/4) unevaluated, and the expand() of the reference's symbolic
         // stage then leaves terms like exp(g)**(27/2) - exp(9 g)*exp(g)**(9/2) un-merged: it
         // rejects these u although det == 0 (all 18 of the depth-4 stream: p > 0 rejected,

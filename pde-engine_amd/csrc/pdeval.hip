@@ -79,6 +79,8 @@ struct pdeval_ctx {
     int64_t* d_list[PD_N_LISTS] = {};
     int32_t* d_counts = nullptr;
     uint8_t* d_pstate = nullptr;    // point-stage state, capacity cap
+    int32_t* d_dec = nullptr;       // decoded programs of the lean grid passes, dec_cap words
+    int64_t dec_cap = 0;
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
     double* d_noise = nullptr;      // fp64 noise bounds at the reference points, cap * 4
     T2Acc* d_t2acc = nullptr;       // tier-2 accumulators, cap entries, zero between launches
@@ -384,6 +386,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     for (int64_t* l : c->d_list)
         if (l) (void)hipFree(l);
     if (c->d_pstate) (void)hipFree(c->d_pstate);
+    if (c->d_dec) (void)hipFree(c->d_dec);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
     if (c->d_t2acc) (void)hipFree(c->d_t2acc);
@@ -529,6 +532,19 @@ static void copy_constants(const pdeval_ctx* c, KernelArgs& a) {
     }
 }
 
+// the decoded-program array of the lean grid passes: as many words as the batch's programs
+// (grown when a batch outgrows it, like the work lists; never inside a sized call)
+static int ensure_dec(pdeval_ctx* c, int64_t n_words) {
+    if (n_words <= c->dec_cap) return PDEVAL_OK;
+    if (c->d_dec) (void)hipFree(c->d_dec);
+    c->d_dec = nullptr;
+    c->dec_cap = 0;
+    const int64_t cap = n_words < 4096 ? 4096 : n_words;
+    HIPCHK(c, hipMalloc(&c->d_dec, cap * sizeof(int32_t)));
+    c->dec_cap = cap;
+    return PDEVAL_OK;
+}
+
 static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (n <= c->cap) return PDEVAL_OK;
     for (int64_t*& l : c->d_list) {
@@ -649,6 +665,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.pdeep_count = cnt + L_PDEEP;
     a.noise_ref = c->d_noise;
     a.t2acc = c->d_t2acc;
+    a.dec = c->d_dec;
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
     // complex-valued ones -> L_CPLX.  Lanes take the candidates sorted by opcode sequence
@@ -681,6 +698,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 1: programs whose stack fits 2 jets (99 % of force-free depth 4), one wave per
     // candidate; deeper programs go to L_DEFER, tier-1 grid failures to L_ESC
     mark(2);
+    launch_decode(PROB, n, s, a);   // (part of pass 1's time)
+    HIPCHK(c, hipGetLastError());
     launch_grid(PROB, n, s, a, c->d_list[L_SLOW], cnt + L_SLOW);
     HIPCHK(c, hipGetLastError());
     // what the lean pass did not take (normally nothing): the generic kernel, same pass slot
@@ -791,6 +810,8 @@ extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64
     if (params) prm = *params;
     else pdeval_default_params(c->problem, &prm);
     int rc = ensure_scratch(c, n);
+    if (rc) return rc;
+    rc = ensure_dec(c, n_words);
     if (rc) return rc;
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (zero_bits && d_out->verdict_bits)

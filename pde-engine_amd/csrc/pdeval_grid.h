@@ -4,11 +4,11 @@
 // Same arithmetic as validate_kernel<PROB, double, 2, ...> -- the same JetOps calls in the same
 // order, so every residual is bit-identical -- but laid out for the CDNA issue model rather than
 // as one generic kernel:
-//  * the program is checked ONCE per candidate (lean_prescan: opcodes, immediates in bounds,
-//    stack depth 1..2, ends at depth 1) instead of at every opcode of every grid row; the
-//    interpreter then runs with no bounds checks and no stack-depth bookkeeping (the stack is
-//    one LDS slot: every push after the first spills the accumulator there, every binary op
-//    reads it back);
+//  * the program is checked and decoded ONCE per candidate (decode_kernel: opcodes, immediates
+//    in bounds, stack depth, ends at depth 1; instruction lengths, dispatch groups and problem
+//    constants resolved) instead of at every opcode of every grid row; the interpreter then
+//    runs with no bounds checks and no stack-depth bookkeeping (the stack is one LDS slot:
+//    every push after the first spills the accumulator there, every binary op reads it back);
 //  * the reference points (chunk 0) are not part of the loop: pass 0 decided them, so the loop
 //    is rows x row-slices with no per-chunk divisions or point-stage branches;
 //  * 1/y of the lane's ordinate (DIV_Y) is formed once per wave, 1/x once per row (scalar x);
@@ -26,14 +26,11 @@
 
 namespace pd {
 
-// Peephole superinstructions in the lean interpreter (Lean::run): measured and rejected.  On
-// one box (profiles/r03_ab1_*.log, 2^20 candidates) pass 1 took 83.5 ms with them against
-// 77.6 ms without (force-free) and 40.6 against 38.8 ms (Kerr): the extra scalar tests on every
-// opcode cost more than the dispatches they save.  Pass 2's register operand slot (RSLOT) is
-// kept: Kerr pass 2 21.4 -> 18.3 ms, force-free 2.26 -> 2.10 ms.
-#ifndef PD_LEAN_FUSE
-#define PD_LEAN_FUSE 0
-#endif
+// Pass 2's register operand slot (Lean::RSLOT): Kerr pass 2 21.4 -> 18.3 ms, force-free
+// 2.26 -> 2.10 ms (profiles/r03_ab1_*.log; 0 builds the variant without it).  Peephole
+// superinstructions (PUSH_C+MUL_P, any op + MULC / ADDC in one dispatch) were measured slower
+// on the same box (pass 1 83.5 vs 77.6 ms force-free, 40.6 vs 38.8 ms Kerr): the extra scalar
+// tests on every opcode cost more than the dispatches they saved; removed.
 #ifndef PD_LEAN_RSLOT
 #define PD_LEAN_RSLOT 1
 #endif
@@ -61,36 +58,81 @@ constexpr uint64_t kPOpMask = op_bit(PDOP_ADD_P) | op_bit(PDOP_SUB_P) | op_bit(P
 constexpr uint64_t kVarMask = op_bit(PDOP_MUL_X) | op_bit(PDOP_MUL_Y) | op_bit(PDOP_DIV_X) |
                               op_bit(PDOP_DIV_Y);
 
-// Program words [1, plen) run by Lean::run with a MAXD-jet stack?  Wave-uniform, scalar only.
-template <int MAXD> __device__ __forceinline__ bool lean_prescan(const int32_t* prog, int plen) {
-    if (plen < 2) return false;
-    int pc = 1, d = 0;
-    while (pc < plen) {
-        const uint32_t w = rd_word(prog + pc);
+// ---- pre-decoded programs.  The lean interpreter's per-opcode scalar work -- instruction
+// length (immediate? double-double?), the next word's address, "was that the last opcode",
+// the dispatch-group tests, the problem-constant lookup of an immediate -- is the same for
+// every grid row of a candidate.  decode_kernel does it once per candidate, before pass 1, into
+// a word array laid out like the programs (same offsets, n_words long):
+//   at the header position     0 and the program's true stack depth in bits 8-15, or 0xff if
+//                              the lean passes cannot take it (lean_prescan<3> fails)
+//   at each opcode position    op (bits 0-7), the word's own bits 8-16 (POWN / coordinate power
+//                              n, axis), the dispatch group (17-19), last-opcode bit (20), the
+//                              distance to the next opcode (21-23: 1, 3 or 5)
+//   after an immediate opcode  the immediate as a double (low word first), a problem constant
+//                              (PDEVAL_IMM_PRM) already resolved to the grid stage's value
+// The lean passes then read only the decoded array.
+enum : uint32_t { DG_PUSH = 0, DG_CHEAP = 1, DG_POP = 2, DG_BIN = 3, DG_VAR = 4, DG_OTHER = 5 };
+__device__ __forceinline__ uint32_t dec_group(uint64_t b) {
+    if (b & kPushMask) return DG_PUSH;
+    if (b & kCheapMask) return DG_CHEAP;
+    if (b & kPOpMask) return DG_POP;
+    if (b & kBinMask) return DG_BIN;
+    if (b & kVarMask) return DG_VAR;
+    return DG_OTHER;
+}
+
+template <int PROB>
+__global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
+    const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cand >= a.n) return;
+    const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
+    if (!(beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24))) return;   // slow path
+    const int32_t* prog = a.ops + beg;
+    int32_t* dec = a.dec + beg;
+    const int plen = (int)(end - beg);
+    const uint32_t hdr = (uint32_t)prog[0];
+    bool ok = plen >= 2 && (hdr & 0xffu) == 0u && !(hdr & PDEVAL_FLAG_COMPLEX);
+    int pc = 1, d = 0, dmax = 0, last = -1;
+    while (ok && pc < plen) {
+        const uint32_t w = (uint32_t)prog[pc];
         const uint32_t op = w & 0xffu;
-        if (op >= 64u) return false;
+        if (op >= 64u) { ok = false; break; }
         const uint64_t b = 1ull << op;
         const int len = (kImmMask & b) ? ((w & PDEVAL_IMM_DD) ? 5 : 3) : 1;
-        if (pc + len > plen) return false;
-        // POWN beyond 8 takes the generic kernel (see pown_lean; none in the depth-4 streams)
-        if (op == PDOP_POWN && ((w >> 8) & 0xffu) > 8u) return false;
-        // a constant of the problem (PDEVAL_IMM_PRM): a valid descriptor, never an exponent
-        if ((kImmMask & b) && (w & PDEVAL_IMM_PRM) &&
-            (op == PDOP_POW || (w & PDEVAL_IMM_DD) || rd_word(prog + pc + 1) > 15u))
-            return false;
+        if (pc + len > plen) { ok = false; break; }
+        if (op == PDOP_POWN && ((w >> 8) & 0xffu) > 8u) { ok = false; break; }   // (pown_lean)
         if (kPushMask & b) {
-            if (++d > MAXD) return false;
+            if (++d > 3) { ok = false; break; }
+            dmax = max(dmax, d);
         } else if (kBinMask & b) {
-            if (d < 2) return false;
+            if (d < 2) { ok = false; break; }
             --d;
         } else if (kUnaryMask & b) {
-            if (d < 1) return false;
+            if (d < 1) { ok = false; break; }
         } else {
-            return false;
+            ok = false;
+            break;
         }
+        if (kImmMask & b) {
+            double v;
+            if (w & PDEVAL_IMM_PRM) {
+                const uint32_t desc = (uint32_t)prog[pc + 1];
+                if (op == PDOP_POW || (w & PDEVAL_IMM_DD) || desc > 15u) { ok = false; break; }
+                v = prm_value(a.prm_grid, desc);
+            } else {
+                v = __hiloint2double(prog[pc + 2], prog[pc + 1]);
+            }
+            dec[pc + 1] = __double2loint(v);
+            dec[pc + 2] = __double2hiint(v);
+        }
+        dec[pc] = (int32_t)(op | (w & 0x1ff00u & ((kImmMask & b) ? 0u : ~0u)) | (dec_group(b) << 17) |
+                            ((uint32_t)len << 21));
+        last = pc;
         pc += len;
     }
-    return d == 1;
+    ok = ok && d == 1 && last >= 0;
+    if (ok) dec[last] |= (int32_t)(1u << 20);
+    dec[0] = ok ? (int32_t)((uint32_t)dmax << 8) : (int32_t)0xff;
 }
 
 // W sample points per lane (W grid rows per dispatch of one opcode): the opcode decode, the
@@ -120,45 +162,34 @@ template <int K, int W, int MAXD> struct Lean {
             for (int c = 0; c < NCJ; ++c) t[w].c[c] = stk[(w * NCJ + c) * 64 + lane];
     }
 
-    // Evaluate a prescanned program at (x[w], y), w < W; inv_x = 1/x, inv_y = 1/y (as rcp()
-    // forms them).  x[] is wave-uniform (one grid row each), y is the lane's ordinate.
-    static __device__ __forceinline__ void run(const int32_t* prog, int plen, const double (&x)[W], double y,
+    // Evaluate a decoded program (decode_kernel; `dec` at the program's header word) at
+    // (x[w], y), w < W; inv_x = 1/x, inv_y = 1/y (as rcp() forms them).  x[] is wave-uniform
+    // (one grid row each), y is the lane's ordinate.
+    static __device__ __forceinline__ void run(const int32_t* dec, const double (&x)[W], double y,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
-                                               double* stk, int lane, const PrmTab<double>& P) {
+                                               double* stk, int lane) {
         // MAXD = 3 (pass 2): the upper of the two operand slots lives in VGPRs, the lower in
         // LDS -- two LDS slots of W = 2 Kerr jets (12 KiB per wave) held pass 2 at ~3 waves
         // per SIMD; with one, VGPRs set the occupancy
         J reg[RSLOT ? W : 1];
         int pc = 1;
-        uint32_t w = rd_word(prog + 1);
+        uint32_t w = rd_word(dec + 1);
         bool first = true;
         int d = 0;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
         for (;;) {
             const uint32_t op = w & 0xffu;
-            const bool has_imm = (kImmMask >> op) & 1u;
-            const int npc = pc + (has_imm ? ((w & PDEVAL_IMM_DD) ? 5 : 3) : 1);
-            const bool more = npc < plen;
+            const uint32_t grp = (w >> 17) & 7u;
+            const bool more = !((w >> 20) & 1u);
+            const int npc = pc + (int)((w >> 21) & 7u);
             // the next opcode word is fetched before this op's arithmetic (its scalar-load
             // latency hides under it); the last op re-reads its own word
-            const uint32_t wn = rd_word(prog + (more ? npc : pc));
+            const uint32_t wn = rd_word(dec + (more ? npc : pc));
             const int pn = (int)((w >> 8) & 0xffu);   // POWN exponent / coordinate power n
             const bool on_y = (w >> 16) & 1u;         // coordinate-power axis
-            // peephole superinstructions (no change to the program format, the same arithmetic
-            // in the same order, one dispatch instead of two):
-            //  * PUSH_C c followed by MUL_P / MUL_X / MUL_Y pushes c * v^n (c * x, c * y): the
-            //    coordinate jet scaled by c, the products the two opcodes form on a constant jet;
-            //  * any other opcode followed by MULC or ADDC: the scale / constant add is applied
-            //    at the end of the same iteration (sfx below).
-            // Kerr programs: 14 % PUSH_C+MUL_* pairs, 21 % MULC / ADDC.  (Off: PD_LEAN_FUSE.)
-            const uint32_t opn = wn & 0xffu;
-            const bool fuse = PD_LEAN_FUSE && more && op == PDOP_PUSH_C &&
-                              (opn == PDOP_MUL_P || opn == PDOP_MUL_X || opn == PDOP_MUL_Y);
-            const bool sfx = PD_LEAN_FUSE && more && !fuse && (opn == PDOP_MULC || opn == PDOP_ADDC);
-            // dispatch: a tree of wave-uniform bit tests over opcode groups (most frequent
-            // first), each a structured if/else -- a flat switch lowers to a compare tree whose
-            // unstructured joins the structurizer turns into extra flow masks and copies
-            const uint64_t b = 1ull << op;
-            if (b & kPushMask) {
+            // dispatch: the decoded group, then the opcode, each a structured if/else (a flat
+            // switch lowers to a compare tree whose unstructured joins the structurizer turns
+            // into extra flow masks and copies)
+            if (grp == DG_PUSH) {
                 if (!first) {
                     if (RSLOT && d == 2) {
 #pragma unroll
@@ -188,52 +219,20 @@ template <int K, int W, int MAXD> struct Lean {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
                 } else {
-                    const double c = rd_immp(prog + pc + 1, w, P);
-                    if (!fuse) {
+                    const double c = rd_imm(dec + pc + 1);
 #pragma unroll
-                        for (int q = 0; q < W; ++q) O::set_const(acc[q], c);
-                    } else if (opn == PDOP_MUL_X) {
-#pragma unroll
-                        for (int q = 0; q < W; ++q) {
-                            O::set_var(acc[q], x[q], 0);
-                            O::scale(acc[q], c);
-                        }
-                    } else if (opn == PDOP_MUL_Y) {
-#pragma unroll
-                        for (int q = 0; q < W; ++q) {
-                            O::set_var(acc[q], y, 1);
-                            O::scale(acc[q], c);
-                        }
-                    } else {
-                        const int pn2 = (int)((wn >> 8) & 0xffu);
-                        double pk[K + 1];
-                        if ((wn >> 16) & 1u) {
-                            O::pcoefs(y, pn2, pk);
-#pragma unroll
-                            for (int q = 0; q < W; ++q) {
-                                O::template set_p<1>(acc[q], pk);
-                                O::scale(acc[q], c);
-                            }
-                        } else {
-#pragma unroll
-                            for (int q = 0; q < W; ++q) {
-                                O::pcoefs(x[q], pn2, pk);
-                                O::template set_p<0>(acc[q], pk);
-                                O::scale(acc[q], c);
-                            }
-                        }
-                    }
+                    for (int q = 0; q < W; ++q) O::set_const(acc[q], c);
                 }
-            } else if (b & kCheapMask) {
+            } else if (grp == DG_CHEAP) {
                 if (op == PDOP_ADDC) {
-                    const double c = rd_immp(prog + pc + 1, w, P);
+                    const double c = rd_imm(dec + pc + 1);
 #pragma unroll
                     for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
                 } else if (op == PDOP_NEG) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], -1.0);
                 } else if (op == PDOP_MULC) {
-                    const double c = rd_immp(prog + pc + 1, w, P);
+                    const double c = rd_imm(dec + pc + 1);
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], c);
                 } else if (op == PDOP_ADD_X) {
@@ -261,7 +260,7 @@ template <int K, int W, int MAXD> struct Lean {
                         acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + (-1.0);
                     }
                 }
-            } else if (b & kPOpMask) {
+            } else if (grp == DG_POP) {
                 double pk[K + 1];
                 if (on_y) {
                     O::pcoefs(y, pn, pk);
@@ -274,7 +273,7 @@ template <int K, int W, int MAXD> struct Lean {
                         O::template p_op<0>(op, acc[q], pk);
                     }
                 }
-            } else if (b & kBinMask) {
+            } else if (grp == DG_BIN) {
                 const double* src = stk + (MAXD == 2 || RSLOT ? 0 : d - 2) * SLOT;
                 const bool from_reg = RSLOT && d == 3;
                 --d;
@@ -296,7 +295,7 @@ template <int K, int W, int MAXD> struct Lean {
                     else if (op == PDOP_RDIV) O::rdiv(l, acc[q]);
                     else O::rsub(l, acc[q]);
                 }
-            } else if (b & kVarMask) {
+            } else if (grp == DG_VAR) {
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
                     if (op == PDOP_DIV_Y) div_var(acc[q], y, inv_y, 1);
@@ -308,36 +307,18 @@ template <int K, int W, int MAXD> struct Lean {
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
                     if (op == PDOP_EXP) O::expj(acc[q]);
-                    else if (op == PDOP_POW) O::powa(acc[q], rd_imm(prog + pc + 1));
-                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], rd_immp(prog + pc + 1, w, P));
+                    else if (op == PDOP_POW) O::powa(acc[q], rd_imm(dec + pc + 1));
+                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], rd_imm(dec + pc + 1));
                     else if (op == PDOP_SQRT) O::sqrtj(acc[q]);
                     else if (op == PDOP_LOG) O::logj(acc[q]);
                     else if (op == PDOP_POWN) pown_lean(acc[q], pn);
                     else absj<K>(acc[q]);
                 }
             }
-            if (sfx) {   // ... MULC c / ADDC c
-                const double c = rd_immp(prog + npc + 1, wn, P);
-                if (opn == PDOP_MULC) {
-#pragma unroll
-                    for (int q = 0; q < W; ++q) O::scale(acc[q], c);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
-                }
-            }
-            int pc_next = npc;
-            uint32_t w_next = wn;
-            bool more_next = more;
-            if (fuse || sfx) {   // skip the fused second opcode (MULC / ADDC carry an immediate)
-                pc_next = npc + (sfx ? ((wn & PDEVAL_IMM_DD) ? 5 : 3) : 1);
-                more_next = pc_next < plen;
-                w_next = rd_word(prog + (more_next ? pc_next : pc));
-            }
-            if (!more_next) break;
+            if (!more) break;
             first = false;
-            pc = pc_next;
-            w = w_next;
+            pc = npc;
+            w = wn;
         }
     }
 
@@ -474,7 +455,6 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
     const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24);
     const int32_t* prog = a.ops + (in_bounds ? beg : 0);
-    const int plen = __builtin_amdgcn_readfirstlane(in_bounds ? (int)(end - beg) : 0);
     const uint32_t hdr = in_bounds ? rd_word(prog) : 0xffu;
     const uint8_t ps = (uint8_t)__builtin_amdgcn_readfirstlane((int)a.pstate[cand]);
     if (ps & P0_CPLX) return;                                    // the complex passes take it
@@ -484,7 +464,12 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
         if (lane == 0) list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
         return;
     }
-    if (!slow) slow = !lean_prescan<MAXD>(prog, plen);
+    // the decoded program (decode_kernel, run before pass 1): 0xff = not for the lean passes;
+    // its true stack depth must fit this pass's slots
+    if (!slow) {
+        const uint32_t dh = rd_word(a.dec + beg);
+        slow = (dh & 0xffu) != 0u || (int)((dh >> 8) & 0xffu) > MAXD;
+    }
     if (slow) {
         if (lane == 0) list_append(slow_list, slow_count, a.list_capacity, cand);
         return;
@@ -530,7 +515,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             constexpr bool kv_late = W > 2 || (MAXD == 2 && PD_KV_LATE) || (MAXD > 2 && PD_KV_LATE_DEEP);
             if constexpr (!kv_late) load_kv();
             J u[W];
-            L::run(prog, plen, x, y, inv_x, inv_y, u, stk, lane, a.prm_grid);
+            L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane);
             if constexpr (kv_late) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {

@@ -18,6 +18,14 @@ void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                            (grid_lds<PDEVAL_PROBLEM_KERR, 2>(PD_GRID_WPB)), s, a, slow_list, slow_count);
 }
 
+void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a) {
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE)
+        hipLaunchKernelGGL((decode_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((decode_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(256), 0, s, a);
+}
+
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
                       int64_t* slow_list, int32_t* slow_count) {
     if (problem == PDEVAL_PROBLEM_FORCE_FREE)

@@ -72,6 +72,8 @@ struct KernelArgs {
     double* noise_ref;          // n * n_ref fp64 noise bounds at the reference points (point stage)
     struct T2Acc* t2acc;        // tier 2: one accumulator per list entry (pdeval_tier2.h), zeroed
     const int32_t* perm;        // order of pass 0 and the tier-B collect pass (pdeval_sort.hip), or NULL
+    int32_t* dec;               // n_words: the programs pre-decoded for the lean grid passes
+                                // (pdeval_grid.h decode_kernel), or NULL
     // the problem's constants per stage (PDEVAL_IMM_PRM; Kerr M, a): point stage (fp64 and
     // double-double) and the constant test / grid stage
     PrmTab<double> prm_pt, prm_grid;

@@ -18,6 +18,8 @@ void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a
                        int plen, double* out, uint8_t* state);
 // the lean grid passes (pdeval_grid.hip): pass 1 over all n candidates (one wave each, stack
 // <= 2), pass 2 persistent over the stack-3 list a.list (64-thread blocks)
+// decode every program for the lean passes (pdeval_grid.h decode_kernel) into a.dec
+void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a);
 void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                  int64_t* slow_list, int32_t* slow_count);
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,

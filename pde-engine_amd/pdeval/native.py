@@ -123,6 +123,8 @@ def sympy_canonical(e: sp.Basic) -> str:
         return e.name
     if e is sp.E:
         return 'E(1)'
+    if e is sp.I:
+        return 'I'
     if e.is_Add or e.is_Mul:
         return ('A(' if e.is_Add else 'M(') + ','.join(sorted(sympy_canonical(a) for a in e.args)) + ')'
     if e.is_Pow:
