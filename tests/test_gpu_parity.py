@@ -64,13 +64,13 @@ def _cmp_device_oracle(ctx, pd_, strings):
     # grid counts: equal for every candidate, exactly, except
     #  * a constant u (ZERO_GRADIENT, decided before the grid): its residual is rounding noise
     #    (or exactly 0, by evaluation order), its counts are reported only;
-    #  * the force-free candidates listed in golden_data.FF_COUNT_SLACK (measured): tier-1
+    #  * the candidates listed in golden_data.FF_COUNT_SLACK / KERR_COUNT_SLACK (measured): tier-1
     #    counts of point rejects near tau_grid, and jets overflowing near the 2^160 guard --
     #    within the listed per-candidate amounts
     st = dev['status']
     bad = []
     for i in np.flatnonzero(((dev['n_bad'] != ora['n_bad']) | (dev['n_nonfinite'] != ora['n_nonfinite'])) & (st != 3)):
-        nb, nf = G.FF_COUNT_SLACK.get(strings[i], (0, 0)) if pd_.problem_id == 0 else (0, 0)
+        nb, nf = (G.FF_COUNT_SLACK if pd_.problem_id == 0 else G.KERR_COUNT_SLACK).get(strings[i], (0, 0))
         if abs(int(dev['n_bad'][i]) - int(ora['n_bad'][i])) > nb or \
                 abs(int(dev['n_nonfinite'][i]) - int(ora['n_nonfinite'][i])) > nf:
             bad.append((strings[i], int(st[i]), int(dev['n_bad'][i]), int(ora['n_bad'][i]),
