@@ -43,7 +43,8 @@ enum {
     L_ESC_C_DEEP = 12,  // complex tier 2, stack 5..8
     L_SLOW = 13,      // lean grid pass -> the generic stack-2 kernel (malformed / undecided)
     L_SLOW2 = 14,     // lean stack-3 pass -> the generic stack-3 kernel
-    PD_N_LISTS = 15
+    L_SLOW_C = 15,    // lean complex pass -> the generic complex stack-2 kernel
+    PD_N_LISTS = 16
 };
 
 namespace {
@@ -86,6 +87,7 @@ struct pdeval_ctx {
     T2Acc* d_t2acc = nullptr;       // tier-2 accumulators, cap entries, zero between launches
     // shape sort of the batch (pdeval_sort.hip): keys 2 x cap, permutation 2 x cap, scratch
     bool sort = true;               // env PDEVAL_SORT=0 turns it off (measurements)
+    bool lean_cplx = true;          // env PDEVAL_LEAN_CPLX=0: the generic complex pass (A/B)
     uint64_t* d_skeys = nullptr;
     int32_t* d_sidx = nullptr;
     void* d_stemp = nullptr;
@@ -360,6 +362,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     hipError_t e;
     if ((e = hipSetDevice(device_id)) != hipSuccess) return fail("hipSetDevice", e);
     if (const char* v = getenv("PDEVAL_SORT")) c->sort = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_LEAN_CPLX")) c->lean_cplx = atoi(v) != 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     if ((e = hipMalloc(&c->d_gx, 2 * nx * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
@@ -724,8 +727,17 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         // complex passes: candidates not real at the reference point, in complex arithmetic
         // (SymPy evaluates the point exactly, in the complex field: validator.py:363-402)
         mark(5);
-        hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3(pgrid), dim3(64),
-                           (stack_lds<cplx, K, 2>(1)), s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C));
+        // the lean interpreter in complex arithmetic over the decoded programs; what it does not
+        // take (point stage undecided, malformed) the generic complex kernel drains
+        if (c->lean_cplx) {
+            launch_grid_cplx(pgrid, s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C), c->d_list[L_SLOW_C], cnt + L_SLOW_C);
+            HIPCHK(c, hipGetLastError());
+            hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
+                               dim3(64), (stack_lds<cplx, K, 2>(1)), s, follow(L_SLOW_C, L_CPLX_DEEP, L_ESC_C));
+        } else {
+            hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3(pgrid), dim3(64),
+                               (stack_lds<cplx, K, 2>(1)), s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C));
+        }
         HIPCHK(c, hipGetLastError());
         mark(6);
         hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),

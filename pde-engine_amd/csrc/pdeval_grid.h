@@ -72,8 +72,10 @@ constexpr uint64_t kVarMask = op_bit(PDOP_MUL_X) | op_bit(PDOP_MUL_Y) | op_bit(P
 //                              (PDEVAL_IMM_PRM) already resolved to the grid stage's value
 // The lean passes then read only the decoded array.
 enum : uint32_t { DG_PUSH = 0, DG_CHEAP = 1, DG_POP = 2, DG_BIN = 3, DG_VAR = 4, DG_OTHER = 5 };
+__device__ __forceinline__ double re_part(double v) { return v; }
+__device__ __forceinline__ double re_part(cplx v) { return v.re; }
 __device__ __forceinline__ uint32_t dec_group(uint64_t b) {
-    if (b & kPushMask) return DG_PUSH;
+    if (b & (kPushMask | op_bit(PDOP_PUSH_I))) return DG_PUSH;
     if (b & kCheapMask) return DG_CHEAP;
     if (b & kPOpMask) return DG_POP;
     if (b & kBinMask) return DG_BIN;
@@ -91,7 +93,7 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     int32_t* dec = a.dec + beg;
     const int plen = (int)(end - beg);
     const uint32_t hdr = (uint32_t)prog[0];
-    bool ok = plen >= 2 && (hdr & 0xffu) == 0u && !(hdr & PDEVAL_FLAG_COMPLEX);
+    bool ok = plen >= 2 && (hdr & 0xffu) == 0u;   // (COMPLEX programs: the lean complex pass)
     int pc = 1, d = 0, dmax = 0, last = -1;
     while (ok && pc < plen) {
         const uint32_t w = (uint32_t)prog[pc];
@@ -101,7 +103,7 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
         const int len = (kImmMask & b) ? ((w & PDEVAL_IMM_DD) ? 5 : 3) : 1;
         if (pc + len > plen) { ok = false; break; }
         if (op == PDOP_POWN && ((w >> 8) & 0xffu) > 8u) { ok = false; break; }   // (pown_lean)
-        if (kPushMask & b) {
+        if ((kPushMask | op_bit(PDOP_PUSH_I)) & b) {
             if (++d > 3) { ok = false; break; }
             dmax = max(dmax, d);
         } else if (kBinMask & b) {
@@ -139,23 +141,23 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
 // dispatch branches and the immediate loads are paid once for W jets.  Force-free runs W = 1
 // (two 15-coefficient jets per operand would not fit 128 VGPRs); Kerr's 6-coefficient jets run
 // W = 2.  For every point the arithmetic is the same JetOps sequence as at W = 1.
-template <int K, int W, int MAXD> struct Lean {
-    using O = JetOps<double, K>;
+template <class T, int K, int W, int MAXD> struct Lean {
+    using O = JetOps<T, K>;
     using J = typename O::J;
     static constexpr int NCJ = nc(K);
 
-    static constexpr int SLOT = W * NCJ * 64;   // doubles per operand slot
+    static constexpr int SLOT = W * NCJ * 64;   // T values per operand slot
     static constexpr bool RSLOT = PD_LEAN_RSLOT && MAXD == 3;   // operand slot 1 in registers (run below)
     static constexpr int LDS_SLOTS = RSLOT ? 1 : MAXD - 1;
 
     // LDS operand slot of one wave: [w][coef][lane]
-    static __device__ __forceinline__ void store(double* stk, int lane, const J (&t)[W]) {
+    static __device__ __forceinline__ void store(T* stk, int lane, const J (&t)[W]) {
 #pragma unroll
         for (int w = 0; w < W; ++w)
 #pragma unroll
             for (int c = 0; c < NCJ; ++c) stk[(w * NCJ + c) * 64 + lane] = t[w].c[c];
     }
-    static __device__ __forceinline__ void load(const double* stk, int lane, J (&t)[W]) {
+    static __device__ __forceinline__ void load(const T* stk, int lane, J (&t)[W]) {
 #pragma unroll
         for (int w = 0; w < W; ++w)
 #pragma unroll
@@ -167,7 +169,7 @@ template <int K, int W, int MAXD> struct Lean {
     // (one grid row each), y is the lane's ordinate.
     static __device__ __forceinline__ void run(const int32_t* dec, const double (&x)[W], double y,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
-                                               double* stk, int lane) {
+                                               T* stk, int lane) {
         // MAXD = 3 (pass 2): the upper of the two operand slots lives in VGPRs, the lower in
         // LDS -- two LDS slots of W = 2 Kerr jets (12 KiB per wave) held pass 2 at ~3 waves
         // per SIMD; with one, VGPRs set the occupancy
@@ -218,46 +220,51 @@ template <int K, int W, int MAXD> struct Lean {
                 } else if (op == PDOP_PUSH_Y) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
+                } else if (Real<T>::cplx_pass && op == PDOP_PUSH_I) {
+                    if constexpr (Real<T>::cplx_pass) {
+#pragma unroll
+                        for (int q = 0; q < W; ++q) O::set_const(acc[q], imag_unit<T>());
+                    }
                 } else {
                     const double c = rd_imm(dec + pc + 1);
 #pragma unroll
-                    for (int q = 0; q < W; ++q) O::set_const(acc[q], c);
+                    for (int q = 0; q < W; ++q) O::set_const(acc[q], cvt<T>(c));
                 }
             } else if (grp == DG_CHEAP) {
                 if (op == PDOP_ADDC) {
                     const double c = rd_imm(dec + pc + 1);
 #pragma unroll
-                    for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + c;
+                    for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + cvt<T>(c);
                 } else if (op == PDOP_NEG) {
 #pragma unroll
-                    for (int q = 0; q < W; ++q) O::scale(acc[q], -1.0);
+                    for (int q = 0; q < W; ++q) O::scale(acc[q], from_real<T>(-1.0));
                 } else if (op == PDOP_MULC) {
                     const double c = rd_imm(dec + pc + 1);
 #pragma unroll
-                    for (int q = 0; q < W; ++q) O::scale(acc[q], c);
+                    for (int q = 0; q < W; ++q) O::scale(acc[q], cvt<T>(c));
                 } else if (op == PDOP_ADD_X) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        acc[q].c[0] = acc[q].c[0] + x[q];
-                        acc[q].c[ji(1, 0)] = acc[q].c[ji(1, 0)] + 1.0;
+                        acc[q].c[0] = acc[q].c[0] + cvt<T>(x[q]);
+                        acc[q].c[ji(1, 0)] = acc[q].c[ji(1, 0)] + from_real<T>(1.0);
                     }
                 } else if (op == PDOP_SUB_X) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        acc[q].c[0] = acc[q].c[0] + (-x[q]);
-                        acc[q].c[ji(1, 0)] = acc[q].c[ji(1, 0)] + (-1.0);
+                        acc[q].c[0] = acc[q].c[0] + cvt<T>(-x[q]);
+                        acc[q].c[ji(1, 0)] = acc[q].c[ji(1, 0)] + from_real<T>(-1.0);
                     }
                 } else if (op == PDOP_ADD_Y) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        acc[q].c[0] = acc[q].c[0] + y;
-                        acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + 1.0;
+                        acc[q].c[0] = acc[q].c[0] + cvt<T>(y);
+                        acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + from_real<T>(1.0);
                     }
                 } else {
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        acc[q].c[0] = acc[q].c[0] + (-y);
-                        acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + (-1.0);
+                        acc[q].c[0] = acc[q].c[0] + cvt<T>(-y);
+                        acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + from_real<T>(-1.0);
                     }
                 }
             } else if (grp == DG_POP) {
@@ -274,7 +281,7 @@ template <int K, int W, int MAXD> struct Lean {
                     }
                 }
             } else if (grp == DG_BIN) {
-                const double* src = stk + (MAXD == 2 || RSLOT ? 0 : d - 2) * SLOT;
+                const T* src = stk + (MAXD == 2 || RSLOT ? 0 : d - 2) * SLOT;
                 const bool from_reg = RSLOT && d == 3;
                 --d;
                 // one operand jet at a time: W > 2 would not hold W operand jets beside the
@@ -308,7 +315,7 @@ template <int K, int W, int MAXD> struct Lean {
                 for (int q = 0; q < W; ++q) {
                     if (op == PDOP_EXP) O::expj(acc[q]);
                     else if (op == PDOP_POW) O::powa(acc[q], rd_imm(dec + pc + 1));
-                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], rd_imm(dec + pc + 1));
+                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], cvt<T>(rd_imm(dec + pc + 1)));
                     else if (op == PDOP_SQRT) O::sqrtj(acc[q]);
                     else if (op == PDOP_LOG) O::logj(acc[q]);
                     else if (op == PDOP_POWN) pown_lean(acc[q], pn);
@@ -346,15 +353,16 @@ template <int K, int W, int MAXD> struct Lean {
 
     // JetOps::div_var with the reciprocal supplied (identical arithmetic: qdiv(s, v, 1/v))
     static __device__ __forceinline__ void div_var(J& t, double v, double inv, int axis) {
+        const T vv = cvt<T>(v), iv = cvt<T>(inv);
 #pragma unroll
         for (int d = 0; d <= K; ++d) {
 #pragma unroll
             for (int j = 0; j <= d; ++j) {
                 const int i = d - j;
-                double s = t.c[ji(i, j)];
+                T s = t.c[ji(i, j)];
                 if (axis == 0 && i > 0) s = s - t.c[ji(i - 1, j)];
                 if (axis == 1 && j > 0) s = s - t.c[ji(i, j - 1)];
-                t.c[ji(i, j)] = qdiv(s, v, inv);
+                t.c[ji(i, j)] = qdiv(s, vv, iv);
             }
         }
     }
@@ -439,27 +447,30 @@ template <int PROB, int MAXD> constexpr int grid_w() {
 }
 template <int PROB> constexpr int grid_k() { return PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2; }
 // dynamic LDS of one block of `waves` waves: the LDS operand slots (Lean::LDS_SLOTS) of W jets
-template <int PROB, int MAXD> constexpr size_t grid_lds(int waves) {
-    return (size_t)waves * Lean<grid_k<PROB>(), grid_w<PROB, MAXD>(), MAXD>::LDS_SLOTS * grid_w<PROB, MAXD>() *
-           nc(grid_k<PROB>()) * 64 * sizeof(double);
+template <int PROB, int MAXD, class T = double> constexpr size_t grid_lds(int waves) {
+    return (size_t)waves * Lean<T, grid_k<PROB>(), grid_w<PROB, MAXD>(), MAXD>::LDS_SLOTS * grid_w<PROB, MAXD>() *
+           nc(grid_k<PROB>()) * 64 * sizeof(T);
 }
 
-// The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots.
-template <int PROB, int MAXD>
-__device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int lane, double* stk,
+// The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots, jets
+// over T: double, or cplx for the force-free candidates not real at p* (the complex pass, whose
+// point stage point_list_kernel<.., cplx> decided).
+template <int PROB, int MAXD, class T = double>
+__device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int lane, T* stk,
                                           int64_t* slow_list, int32_t* slow_count) {
     constexpr int K = grid_k<PROB>();
     constexpr int W = grid_w<PROB, MAXD>();
-    using L = Lean<K, W, MAXD>;
+    constexpr bool CX = Real<T>::cplx_pass;
+    using L = Lean<T, K, W, MAXD>;
     using J = typename L::J;
     const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
     const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24);
     const int32_t* prog = a.ops + (in_bounds ? beg : 0);
     const uint32_t hdr = in_bounds ? rd_word(prog) : 0xffu;
     const uint8_t ps = (uint8_t)__builtin_amdgcn_readfirstlane((int)a.pstate[cand]);
-    if (ps & P0_CPLX) return;                                    // the complex passes take it
+    if (!CX && (ps & P0_CPLX)) return;                           // the complex passes take it
     if ((ps & 3) == P0_REJECT && !a.prm.full_grid) return;      // final after the point stage
-    bool slow = !in_bounds || (hdr & 0xffu) != 0u || (ps & 3) == P0_NONE || (hdr & PDEVAL_FLAG_COMPLEX);
+    bool slow = !in_bounds || (hdr & 0xffu) != 0u || (ps & 3) == P0_NONE || (!CX && (hdr & PDEVAL_FLAG_COMPLEX));
     if (!slow && (int)((hdr >> 8) & 0xffu) > MAXD) {
         if (lane == 0) list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
         return;
@@ -522,14 +533,14 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 if (W > 1 && row + q >= a.nx) break;                     // uniform
                 const int base = a.n_ref + (row + q) * a.ny + sl * 64;   // point index of lane 0
                 PointResult r;
-                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u[q].c, x[q]);
-                else r = kerr_epilogue<double>(u[q].c, kv[q]);
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u[q].c, x[q]);
+                else r = kerr_epilogue<T>(u[q].c, kv[q]);
                 const double qv = scaled(r.res_abs, r.scale);
                 if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {
                         const int rel = a.fp_pts[f] - base;   // uniform
-                        if (rel >= 0 && rel < 64 && lane == rel) a.out.fingerprint[cand * PDEVAL_FP_N + f] = u[q].c[0];
+                        if (rel >= 0 && rel < 64 && lane == rel) a.out.fingerprint[cand * PDEVAL_FP_N + f] = re_part(u[q].c[0]);
                     }
                 }
                 if (r.finite) {
@@ -606,6 +617,28 @@ __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST
     for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
         const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
         grid_body<PROB, 3>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
+    }
+}
+
+// the complex pass: the force-free candidates not real at p* (list a.list = L_CPLX, count
+// *a.list_count), complex jets, persistent one-wave blocks; deeper programs -> a.defer_list,
+// what the lean path does not take -> slow_list (the generic complex kernel drains it)
+#ifndef PD_CPLX_WAVES_PER_SIMD
+#define PD_CPLX_WAVES_PER_SIMD 2
+#endif
+__global__ __launch_bounds__(64, PD_CPLX_WAVES_PER_SIMD) void grid_cplx_kernel(KernelArgs a, int64_t* slow_list,
+                                                                                int32_t* slow_count) {
+#ifndef PD_HOST_SIM
+    extern __shared__ __align__(16) unsigned char pd_lds[];
+#else
+    static unsigned char pd_lds[1];
+#endif
+    cplx* stk = reinterpret_cast<cplx*>(pd_lds);
+    int64_t nwork = (int64_t)(*a.list_count);
+    if (nwork > a.list_capacity) nwork = a.list_capacity;
+    for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+        const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
+        grid_body<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
     }
 }
 

@@ -26,6 +26,11 @@ void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a) {
         hipLaunchKernelGGL((decode_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(256), 0, s, a);
 }
 
+void launch_grid_cplx(unsigned blocks, hipStream_t s, const KernelArgs& a, int64_t* slow_list, int32_t* slow_count) {
+    hipLaunchKernelGGL(grid_cplx_kernel, dim3(blocks), dim3(64), (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(1)), s,
+                       a, slow_list, slow_count);
+}
+
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
                       int64_t* slow_list, int32_t* slow_count) {
     if (problem == PDEVAL_PROBLEM_FORCE_FREE)

@@ -22,6 +22,8 @@ void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a
 void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a);
 void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                  int64_t* slow_list, int32_t* slow_count);
+// the complex pass (force-free): persistent over the list a.list (L_CPLX), complex jets
+void launch_grid_cplx(unsigned blocks, hipStream_t s, const KernelArgs& a, int64_t* slow_list, int32_t* slow_count);
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
                       int64_t* slow_list, int32_t* slow_count);
 // sort the batch by opcode sequence (pdeval_sort.hip): keys/idx hold 2 x n each, the

@@ -32,7 +32,8 @@ MAX_BATCH = 1 << 30          # PDEVAL_MAX_BATCH
 UNIQUE_ID_BYTES = 128
 LIST_NAMES = ('defer_stack3', 'complex', 'defer_stack8', 'tier2', 'tier2_stack3', 'tier2_complex',
               'complex_stack8', 'tier2_stack8', 'point_deep', 'point_dd', 'point_dd_complex',
-              'point_dd_stack8', 'tier2_complex_stack8', 'grid_slow', 'grid_slow_stack3')
+              'point_dd_stack8', 'tier2_complex_stack8', 'grid_slow', 'grid_slow_stack3',
+              'grid_slow_complex')
 N_PASSES = 12
 
 
