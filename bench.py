@@ -81,6 +81,11 @@ def main():
     ap.add_argument('--no-extras', action='store_true',
                     help='skip the early-exit / host-buffer / time-to-solutions legs')
     a = ap.parse_args()
+    if not a.no_extras and int(os.environ.get('WORLD_SIZE', '1')) == 1 and a.problem == 'force_free':
+        # the worker leg's SymPy pool for the strings the native compiler declines: forked now,
+        # before this process touches the GPU (pdeval/hostpool.py)
+        from pdeval import hostpool
+        hostpool.start()
 
     import torch
     import torch.distributed as dist

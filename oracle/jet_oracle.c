@@ -294,7 +294,7 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
         if (allz) r.finite = 0;
     }
     r.grad_zero = cc[IDX(1, 0)] == 0 && cc[IDX(0, 1)] == 0;
-    r.u0 = creal(cc[0]);
+    r.u0 = creal(cc[0]) + 0x1.6a09e667f3bcdp+0 * cimag(cc[0]);   /* fingerprint: Re + sqrt(2) Im */
     return r;
 }
 
@@ -373,7 +373,7 @@ static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, 
     r.grad[1] = (double)cabsq(cq[IDX(0, 1)]);
     r.grad_err[0] = W[IDX(1, 0)];
     r.grad_err[1] = W[IDX(0, 1)];
-    r.u0 = (double)crealq(cq[0]);
+    r.u0 = (double)crealq(cq[0]) + 0x1.6a09e667f3bcdp+0 * (double)cimagq(cq[0]);
     return r;
 }
 

@@ -72,8 +72,6 @@ constexpr uint64_t kVarMask = op_bit(PDOP_MUL_X) | op_bit(PDOP_MUL_Y) | op_bit(P
 //                              (PDEVAL_IMM_PRM) already resolved to the grid stage's value
 // The lean passes then read only the decoded array.
 enum : uint32_t { DG_PUSH = 0, DG_CHEAP = 1, DG_POP = 2, DG_BIN = 3, DG_VAR = 4, DG_OTHER = 5 };
-__device__ __forceinline__ double re_part(double v) { return v; }
-__device__ __forceinline__ double re_part(cplx v) { return v.re; }
 __device__ __forceinline__ uint32_t dec_group(uint64_t b) {
     if (b & (kPushMask | op_bit(PDOP_PUSH_I))) return DG_PUSH;
     if (b & kCheapMask) return DG_CHEAP;
@@ -540,7 +538,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {
                         const int rel = a.fp_pts[f] - base;   // uniform
-                        if (rel >= 0 && rel < 64 && lane == rel) a.out.fingerprint[cand * PDEVAL_FP_N + f] = re_part(u[q].c[0]);
+                        if (rel >= 0 && rel < 64 && lane == rel) a.out.fingerprint[cand * PDEVAL_FP_N + f] = fp_value(u[q].c[0]);
                     }
                 }
                 if (r.finite) {

@@ -493,6 +493,12 @@ constexpr double kHugeJet = 0x1p160;
 // structural: exp(-exp(r/a**2)) has r).  A u that cancels exactly (-x/(1 - x) - 1 + 1/(1 - x))
 // has zero coefficients too, but rounding bounds of the size of its terms: not an underflow.
 constexpr double kTinyJet = 0x1p-900;
+// The fingerprint value of u at a point: u itself, or Re u + sqrt(2) Im u for a complex u -- a
+// complex constant has a flat fingerprint, a purely imaginary non-constant one does not (the
+// host's zero-gradient re-check looks only at flat fingerprints, pdeval/batch.py)
+constexpr double kFpIm = 0x1.6a09e667f3bcdp+0;
+__device__ __forceinline__ double fp_value(double v) { return v; }
+__device__ __forceinline__ double fp_value(cplx v) { return v.re + kFpIm * v.im; }
 template <class T, int NC> __device__ __forceinline__ bool underflowed(const double* m, const double* e) {
     bool t = true;
 #pragma unroll
@@ -983,10 +989,7 @@ void validate_kernel(KernelArgs a) {
 #pragma unroll
                 for (int f = 0; f < PDEVAL_FP_N; ++f)
                     if (p == a.fp_pts[f] && a.out.fingerprint) {
-                        double v;
-                        if constexpr (Real<T>::cplx_pass) v = ((const cplx*)&u.c[0])->re;
-                        else v = *(const double*)&u.c[0];
-                        a.out.fingerprint[cand * PDEVAL_FP_N + f] = v;
+                        a.out.fingerprint[cand * PDEVAL_FP_N + f] = fp_value(u.c[0]);
                     }
             }
             if (active && p < a.n_ref) {

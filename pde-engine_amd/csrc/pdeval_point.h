@@ -65,7 +65,7 @@ template <> __device__ __forceinline__ const PrmTab<dd>& stage_prm<dd>(const Ker
 struct PtEval {
     double res_re, res_im, res_abs;  // residual (hi parts)
     double S, noise;                 // magnitude scale and first-order noise bound
-    double u0;                       // Re u at the point (fingerprint)
+    double u0;                       // fingerprint value at the point (fp_value)
     bool finite, grad_zero;
     bool grad_noise;                 // |u_x|, |u_y| within kappa x their rounding-error bounds
     bool tiny;                       // Kerr: u's jet underflowed (kTinyJet): a passing point
@@ -115,7 +115,7 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
     r.res_re = re_hi(res);
     r.res_im = im_hi(res);
     r.res_abs = mag(res);
-    r.u0 = re_hi(u.c[0]);
+    r.u0 = re_hi(u.c[0]) + kFpIm * im_hi(u.c[0]);   // (fp_value)
     r.grad_zero = is_zero(u.c[ji(1, 0)]) && is_zero(u.c[ji(0, 1)]);
     // coefficient i is within eps * e[i] of exact (first order; dd: dd_unit * e[i])
     const double gk = a.prm.noise_kappa * kEps * unit;

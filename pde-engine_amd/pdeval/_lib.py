@@ -138,11 +138,16 @@ def _ptr(a: Optional[np.ndarray]):
     return None if a is None else a.ctypes.data
 
 
+CONTEXTS_CREATED = 0   # (pdeval.hostpool forks only before the first one: the GPU is then live)
+
+
 class Context:
     """One libpdeval context = one GPU + one problem's sample grid."""
 
     def __init__(self, problem_id: int, device: int = 0, grid: Optional[np.ndarray] = None,
                  kerr: Optional[KerrConstants] = None):
+        global CONTEXTS_CREATED
+        CONTEXTS_CREATED += 1
         lib = load()
         h = C.c_void_p()
         gp = None

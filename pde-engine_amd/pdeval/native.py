@@ -81,7 +81,7 @@ def compile_strings(pd_, strings: Sequence[str], stats: Optional[dict] = None,
     Returns (ops, offsets, notes) with notes[i] = None or the reason a program is a stub.
     With a ``stats`` dict, ``stats['status']`` receives the native compiler's per-string
     status (COMPILE_PARSE marks the strings it could not parse)."""
-    from .problem_defs import compile_strings as sympy_compile
+    from .hostpool import compile_strings as sympy_compile   # (the SymPy pool when it runs)
     ops, off, st = compile_native(pd_.problem_id, strings, threads)
     host = np.flatnonzero(st != COMPILE_OK)
     if stats is not None:

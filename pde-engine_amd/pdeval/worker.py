@@ -103,6 +103,8 @@ def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[s
                      batch_size: int = 4096, device: int = 0, idle_exit_s: Optional[float] = None):
     """Worker process body (one per GPU).  Returns the number of candidates validated."""
     from problems import load_problem
+    from . import hostpool
+    hostpool.start()          # the SymPy pool for declined strings, before the GPU is touched
     problem = load_problem(problem_name)
     validator = problem.validator
     if hasattr(validator, 'device'):

@@ -180,3 +180,21 @@ def test_format_reasons_equals_reason_for(prob):
                        bool(rat[i]), notes[i])[1] for i in range(n)]
     bad = [(i, got[i], want[i]) for i in range(n) if got[i] != want[i]]
     assert not bad, bad[:5]
+
+
+def test_hostpool_compile_equals_in_process():
+    """pdeval.hostpool (the SymPy process pool for declined strings, forked before any GPU
+    use) returns exactly what problem_defs.compile_strings returns in-process."""
+    from pdeval import hostpool
+    strs = [s for s in _stream('force_free_d4_validated.txt.gz')[:40000]]
+    ops, off, st = native.compile_native(0, strs)
+    declined = [s for s, x in zip(strs, st) if x != native.COMPILE_OK][:40]
+    assert declined
+    want = P.compile_strings(P.force_free(), declined)
+    if hostpool.start(2) is None:
+        pytest.skip('the GPU is live in this process: no fork')
+    try:
+        got = hostpool.compile_strings(P.force_free(), declined)
+    finally:
+        hostpool.stop()
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
