@@ -117,6 +117,28 @@ enum : uint32_t {
 enum : uint8_t { P0_NONE = 0, P0_PASS = 1, P0_REJECT = 2, P0_CPLX = 4, P0_PROV = 8, P0_GRAD = 16,
                  P0_DD = 32, P0_CONST = 64, P0_NZ = 128 };
 
+// The one-candidate-per-lane interpreters (ValInterp::run of the double-double point tier,
+// ErrInterp::run_s of the point / tier-2 stages) are force-inlined: as calls, the complex and
+// double-double instances kept their arguments and the by-value kernel arguments they referenced
+// in scratch (dd_point_kernel<0,dd,2>: 2,036 -> 144 B per lane; tier-2 complex 1,744 -> 656 B).
+// PD_DD_INLINE=0 / PD_T2_INLINE=0 give the compiler back the choice (A/B variants).
+#ifndef PD_DD_INLINE
+#define PD_DD_INLINE 1
+#endif
+#ifndef PD_T2_INLINE
+#define PD_T2_INLINE 1
+#endif
+#if PD_DD_INLINE
+#define PD_DD_INLINE_ATTR __forceinline__
+#else
+#define PD_DD_INLINE_ATTR
+#endif
+#if PD_T2_INLINE
+#define PD_T2_INLINE_ATTR __forceinline__
+#else
+#define PD_T2_INLINE_ATTR
+#endif
+
 #define PD_ESC_SHIFT 48
 #define PD_ESC_CAND_MASK ((1ll << PD_ESC_SHIFT) - 1)
 

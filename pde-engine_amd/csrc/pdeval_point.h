@@ -53,6 +53,13 @@ template <> __device__ __forceinline__ dd ref_coord<dd>(const KernelArgs& a, int
     return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3]));
 }
 
+// Kerr operator coefficients at reference point k, double-double (selects, as ref_coord)
+__device__ __forceinline__ void kc_ref_at(const KernelArgs& a, int k, dd (&kc)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        kc[i] = k == 0 ? a.kc_ref[i] : (k == 1 ? a.kc_ref[4 + i] : (k == 2 ? a.kc_ref[8 + i] : a.kc_ref[12 + i]));
+}
+
 // the problem's constants of the point stage (grid = false) or of the constant test / grid stage
 template <class V> __device__ __forceinline__ const PrmTab<V>& stage_prm(const KernelArgs& a, bool grid);
 template <> __device__ __forceinline__ const PrmTab<double>& stage_prm<double>(const KernelArgs& a, bool grid) {
@@ -107,7 +114,11 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
         res = FFEpi<T, false>::eval(u.c, x);
         r.S = FFEpi<double, true>::eval(m, hi_of(x));
     } else {
-        if constexpr (std::is_same<V, dd>::value) res = kerr_lhs<T, dd>(u.c, a.kc_ref + 4 * k, &r.S);
+        if constexpr (std::is_same<V, dd>::value) {
+            dd kcd[4];
+            kc_ref_at(a, k, kcd);
+            res = kerr_lhs<T, dd>(u.c, kcd, &r.S);
+        }
         else res = kerr_lhs<T, double>(u.c, kc, &r.S);
     }
     const double unit = std::is_same<V, dd>::value ? dd_unit() / kEps : 1.0;
@@ -446,7 +457,7 @@ template <class T, int K, int MAXD, class V> struct ValInterp {
     using O = JetOps<T, K>;
     using J = typename O::J;
     template <class STK>
-    static __device__ int run(const int32_t* ops, int pc, int end, V x, V y, J& acc, STK& stk,
+    static __device__ PD_DD_INLINE_ATTR int run(const int32_t* ops, int pc, int end, V x, V y, J& acc, STK& stk,
                               const PrmTab<V>& P) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
@@ -541,7 +552,9 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
     bool rej = false, fin_all = true, nzk = false;
     uint8_t ff = P0_PASS;
     for (int p = 0; p < a.n_ref; ++p) {
-        const dd x = a.ref_xd[p & 3], y = a.ref_yd[p & 3];
+        // (selects, not a.ref_xd[p]: a dynamic index into the by-value kernel arguments made
+        // the compiler copy them to scratch -- ~1.9 KB per lane of this kernel's 2 KB)
+        const dd x = ref_coord<dd>(a, p, 0), y = ref_coord<dd>(a, p, 1);
         typename ValInterp<T, K, MAXD, dd>::J u;
         if (ValInterp<T, K, MAXD, dd>::run(prog, 1, plen, x, y, u, stk, a.prm_pt_dd) != RUN_OK) return P0_NONE;
         double m[NC];
@@ -553,7 +566,9 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
             res = FFEpi<T, false>::eval(u.c, x);
             S = FFEpi<double, true>::eval(m, x.hi);
         } else {
-            res = kerr_lhs<T, dd>(u.c, a.kc_ref + 4 * p, &S);
+            dd kc[4];
+            kc_ref_at(a, p, kc);
+            res = kerr_lhs<T, dd>(u.c, kc, &S);
         }
         const double res_abs = mag(res);
         const double noise = a.noise_ref[cand * a.n_ref + p] * (dd_unit() / kEps);

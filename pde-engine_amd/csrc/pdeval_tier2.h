@@ -211,7 +211,7 @@ template <class T, int K, int MAXD, class V = double> struct ErrInterp {
     // the reference points 4/5, 6/7, 1/3 ... are not doubles, and near a pole of the candidate
     // their rounding is amplified like any other error)
     template <bool VEC, class STK>
-    static __device__ int run_s(const int32_t* ops, int pc, int end, V x, V y, J& acc, double* ea, STK& stk,
+    static __device__ PD_T2_INLINE_ATTR int run_s(const int32_t* ops, int pc, int end, V x, V y, J& acc, double* ea, STK& stk,
                                 const PrmTab<V>& P, double cerr = 0.0) {
         int d = 0;
         if (pc >= end) return RUN_BAD;
