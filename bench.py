@@ -317,9 +317,9 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
     general_method_paper_reproduction.py:1756-1816, queue tuples in -> result tuples out):
     * process_batch, one queue-sized batch at a time (native compile, one device call,
       vectorized reasons, known-solution tags);
-    * process_batches, the worker loop's pipeline (batch k+1 compiles on host threads while
-      batch k is on the device), at the default queue batch and at a larger one -- its result
-      tuples must equal process_batch's;
+    * process_batches, the worker loop's three-stage pipeline (batch k+2 compiles on host
+      threads while batch k+1 is on the device and batch k's tuples are built), at the
+      default queue batch and at larger ones -- its result tuples must equal process_batch's;
     * the inline path: one validate(sympify(s)) per candidate, as the driver's sequential loop
       calls it (:1299-1316), on a seeded sample."""
     import random
@@ -341,7 +341,7 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
     dt = time.perf_counter() - t0
     out['process_batch'] = {'batch': batch, 'seconds': round(dt, 3), 'candidates_per_s': round(len(items) / dt),
                             'valid': sum(1 for t in ref if t[1]), 'paper_tagged': sum(1 for t in ref if t[3])}
-    for b in (batch, pipe_batch):
+    for b in (batch, pipe_batch // 2, pipe_batch):
         t0 = time.perf_counter()
         got = []
         for r in process_batches((items[k:k + b] for k in range(0, len(items), b)), prob.validator, kw, locs,

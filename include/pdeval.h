@@ -132,7 +132,7 @@ enum pdeval_opcode {
                                             residual at a rational point is rational (host
                                             reason strings, validator.py:371-380)      */
 #define PDEVAL_FLAG_NONSMOOTH2D (1u << 19) /* contains Abs and references both coordinates */
-#define PDEVAL_FLAG_UNPROVABLE (1u << 20)  /* u = exp(g)**(p/4), p > 0: the reference's symbolic
+#define PDEVAL_FLAG_UNPROVABLE (1u << 20)  /* u = c*exp(g)**(p/4), p > 0, c a number: the reference's symbolic
                                               stage cannot reduce det to 0 (force-free
                                               validator.py:404-416)       */
 

@@ -266,8 +266,11 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
     }
     if (*rc) return r;
     int fin = 1;
-    for (int i = 0; i < NC(K); ++i) fin = fin && fabs(creal(cc[i])) < 0x1p160 && fabs(cimag(cc[i])) < 0x1p160;
-    /* (the device's jet_coef_ok: below 2^160, so no order-dependent overflow downstream) */
+    /* (the device's jet_coef_ok: below 2^160, so no order-dependent overflow downstream; Kerr:
+     * not u_rx, which its operator does not contain -- kerr_epilogue) */
+    const int mix = (problem == PDEVAL_PROBLEM_FORCE_FREE || !grid) ? -1 : IDX(1, 1);
+    for (int i = 0; i < NC(K); ++i)
+        if (i != mix) fin = fin && fabs(creal(cc[i])) < 0x1p160 && fabs(cimag(cc[i])) < 0x1p160;
     double complex res;
     if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
         res = ff_det_c(cc, x, 0);
@@ -290,7 +293,7 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
     if (problem != PDEVAL_PROBLEM_FORCE_FREE) {
         /* Kerr: a jet exactly 0 to second order is an underflow, not a sample (pdeval_kernels.h) */
         int allz = 1;
-        for (int i = 0; i < NC(K); ++i) allz = allz && cc[i] == 0;
+        for (int i = 0; i < NC(K); ++i) allz = allz && (i == mix || cc[i] == 0);
         if (allz) r.finite = 0;
     }
     r.grad_zero = cc[IDX(1, 0)] == 0 && cc[IDX(0, 1)] == 0;

@@ -1542,12 +1542,22 @@ int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t le
         // SymPy keeps exp(g)**(p/4) unevaluated, and the expand() of the reference's symbolic
         // stage then leaves terms like exp(g)**(27/2) - exp(9 g)*exp(g)**(9/2) un-merged: it
         // rejects these u although det == 0 (all 18 of the depth-4 stream: p > 0 rejected,
-        // p < 0 accepted; tests/golden/ref/ff_d4_exp_quarter.jsonl)
+        // p < 0 accepted; tests/golden/ref/ff_d4_exp_quarter.jsonl), and c*exp(g)**(p/4) for a
+        // number c the same way (det is homogeneous in u; ff_exp_quarter_scaled.jsonl, and a
+        // depth-5 sample candidate, ff_d5_s400.jsonl)
         {
+            auto quarter = [&](int id) {
+                const Node& R = C.N(id);
+                return R.k == POW && C.N(R.a[0]).k == EXP && C.N(R.a[1]).k == NUM && C.N(R.a[1]).r.q == 4 &&
+                       C.N(R.a[1]).r.p > 0;
+            };
             const Node& R = C.N(root);
-            if (R.k == POW && C.N(R.a[0]).k == EXP && C.N(R.a[1]).k == NUM && C.N(R.a[1]).r.q == 4 &&
-                C.N(R.a[1]).r.p > 0)
-                hdr |= PDEVAL_FLAG_UNPROVABLE;
+            bool unp = quarter(root);
+            if (!unp && R.k == MUL && R.a.size() == 2) {
+                for (int j = 0; j < 2; ++j)
+                    if (C.N(R.a[j]).k == NUM && C.N(R.a[j]).r.p != 0 && quarter(R.a[1 - j])) unp = true;
+            }
+            if (unp) hdr |= PDEVAL_FLAG_UNPROVABLE;
         }
         out.clear();
         out.push_back((int32_t)hdr);

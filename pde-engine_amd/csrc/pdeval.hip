@@ -543,7 +543,8 @@ static int ensure_dec(pdeval_ctx* c, int64_t n_words) {
     c->d_dec = nullptr;
     c->dec_cap = 0;
     const int64_t cap = n_words < 4096 ? 4096 : n_words;
-    HIPCHK(c, hipMalloc(&c->d_dec, cap * sizeof(int32_t)));
+    // + 4 words: the lean interpreter reads an opcode word with the two after it (pdeval_grid.h)
+    HIPCHK(c, hipMalloc(&c->d_dec, (cap + 4) * sizeof(int32_t)));
     c->dec_cap = cap;
     return PDEVAL_OK;
 }

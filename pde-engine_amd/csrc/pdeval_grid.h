@@ -72,6 +72,12 @@ constexpr uint64_t kVarMask = op_bit(PDOP_MUL_X) | op_bit(PDOP_MUL_Y) | op_bit(P
 //                              (PDEVAL_IMM_PRM) already resolved to the grid stage's value
 // The lean passes then read only the decoded array.
 enum : uint32_t { DG_PUSH = 0, DG_CHEAP = 1, DG_POP = 2, DG_BIN = 3, DG_VAR = 4, DG_OTHER = 5 };
+#ifndef PD_KERR_NOMIX
+#define PD_KERR_NOMIX 1
+#endif
+#ifndef PD_FUSE_PUSHC
+#define PD_FUSE_PUSHC 1
+#endif
 __device__ __forceinline__ uint32_t dec_group(uint64_t b) {
     if (b & (kPushMask | op_bit(PDOP_PUSH_I))) return DG_PUSH;
     if (b & kCheapMask) return DG_CHEAP;
@@ -125,6 +131,20 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
             dec[pc + 1] = __double2loint(v);
             dec[pc + 2] = __double2hiint(v);
         }
+        // Kerr: PUSH_C c followed by MUL_X / MUL_Y / MUL_P (c x, c y, c x^n: 1.9 of its 13.4
+        // opcodes per depth-4 candidate; force-free has 0.14) decode into one push: the second opcode with the
+        // PUSH group, c as its immediate, the distance over both.  The interpreter runs the
+        // same two JetOps calls (set_const, then the multiply), so the values are the same.
+        if (PD_FUSE_PUSHC && PROB != PDEVAL_PROBLEM_FORCE_FREE && op == PDOP_PUSH_C && pc + len < plen) {
+            const uint32_t w2 = (uint32_t)prog[pc + len];
+            const uint32_t op2 = w2 & 0xffu;
+            if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || op2 == PDOP_MUL_P) {
+                dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << 21));
+                last = pc;
+                pc += len + 1;
+                continue;
+            }
+        }
         dec[pc] = (int32_t)(op | (w & 0x1ff00u & ((kImmMask & b) ? 0u : ~0u)) | (dec_group(b) << 17) |
                             ((uint32_t)len << 21));
         last = pc;
@@ -139,12 +159,22 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
 // dispatch branches and the immediate loads are paid once for W jets.  Force-free runs W = 1
 // (two 15-coefficient jets per operand would not fit 128 VGPRs); Kerr's 6-coefficient jets run
 // W = 2.  For every point the arithmetic is the same JetOps sequence as at W = 1.
+#ifndef PD_LEAN_IMM_PREFETCH
+#define PD_LEAN_IMM_PREFETCH 1
+#endif
 template <class T, int K, int W, int MAXD> struct Lean {
     using O = JetOps<T, K>;
     using J = typename O::J;
     static constexpr int NCJ = nc(K);
 
     static constexpr int SLOT = W * NCJ * 64;   // T values per operand slot
+    // Kerr (K = 2): the mixed coefficient u_rx feeds only itself through every jet operation
+    // and the operator has no mixed term (kerr_epilogue), so it is not stored, not loaded and
+    // forced to 0 after each opcode; the compiler then drops its arithmetic (PD_KERR_NOMIX=0:
+    // the full jets, an A/B variant -- same values of every other coefficient)
+    static constexpr bool NOMIX = PD_KERR_NOMIX && K == 2;
+    static constexpr int MIX = ji(1, 1);
+    static __device__ __forceinline__ bool live(int c) { return !(NOMIX && c == MIX); }
     static constexpr bool RSLOT = PD_LEAN_RSLOT && MAXD == 3;   // operand slot 1 in registers (run below)
     static constexpr int LDS_SLOTS = RSLOT ? 1 : MAXD - 1;
 
@@ -153,13 +183,14 @@ template <class T, int K, int W, int MAXD> struct Lean {
 #pragma unroll
         for (int w = 0; w < W; ++w)
 #pragma unroll
-            for (int c = 0; c < NCJ; ++c) stk[(w * NCJ + c) * 64 + lane] = t[w].c[c];
+            for (int c = 0; c < NCJ; ++c)
+                if (live(c)) stk[(w * NCJ + c) * 64 + lane] = t[w].c[c];
     }
     static __device__ __forceinline__ void load(const T* stk, int lane, J (&t)[W]) {
 #pragma unroll
         for (int w = 0; w < W; ++w)
 #pragma unroll
-            for (int c = 0; c < NCJ; ++c) t[w].c[c] = stk[(w * NCJ + c) * 64 + lane];
+            for (int c = 0; c < NCJ; ++c) t[w].c[c] = live(c) ? stk[(w * NCJ + c) * 64 + lane] : zero<T>();
     }
 
     // Evaluate a decoded program (decode_kernel; `dec` at the program's header word) at
@@ -173,7 +204,11 @@ template <class T, int K, int W, int MAXD> struct Lean {
         // per SIMD; with one, VGPRs set the occupancy
         J reg[RSLOT ? W : 1];
         int pc = 1;
+        // an opcode word and the two after it (its f64 immediate, when it has one) are read
+        // together, one op ahead, so an op's immediate is in SGPRs when its turn comes instead
+        // of costing a dependent scalar load (dec[] is padded by 4 words past its end)
         uint32_t w = rd_word(dec + 1);
+        double imm = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + 2) : 0.0;
         bool first = true;
         int d = 0;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
         for (;;) {
@@ -183,7 +218,10 @@ template <class T, int K, int W, int MAXD> struct Lean {
             const int npc = pc + (int)((w >> 21) & 7u);
             // the next opcode word is fetched before this op's arithmetic (its scalar-load
             // latency hides under it); the last op re-reads its own word
-            const uint32_t wn = rd_word(dec + (more ? npc : pc));
+            const int pn_at = more ? npc : pc;
+            const uint32_t wn = rd_word(dec + pn_at);
+            const double immn = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + pn_at + 1) : 0.0;
+            const double cimm = PD_LEAN_IMM_PREFETCH ? imm : rd_imm(dec + pc + 1);
             const int pn = (int)((w >> 8) & 0xffu);   // POWN exponent / coordinate power n
             const bool on_y = (w >> 16) & 1u;         // coordinate-power axis
             // dispatch: the decoded group, then the opcode, each a structured if/else (a flat
@@ -218,26 +256,44 @@ template <class T, int K, int W, int MAXD> struct Lean {
                 } else if (op == PDOP_PUSH_Y) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
+                } else if (PD_FUSE_PUSHC && K == 2 && (op == PDOP_MUL_X || op == PDOP_MUL_Y || op == PDOP_MUL_P)) {
+                    // a fused PUSH_C c + MUL_* (decode_kernel): the two opcodes' calls
+                    double pk[K + 1];
+                    if (op == PDOP_MUL_P && on_y) O::pcoefs(y, pn, pk);
+#pragma unroll
+                    for (int q = 0; q < W; ++q) {
+                        O::set_const(acc[q], cvt<T>(cimm));
+                        if (op == PDOP_MUL_X) {
+                            O::mul_var(acc[q], x[q], 0);
+                        } else if (op == PDOP_MUL_Y) {
+                            O::mul_var(acc[q], y, 1);
+                        } else if (on_y) {
+                            O::template p_op<1>(PDOP_MUL_P, acc[q], pk);
+                        } else {
+                            O::pcoefs(x[q], pn, pk);
+                            O::template p_op<0>(PDOP_MUL_P, acc[q], pk);
+                        }
+                    }
                 } else if (Real<T>::cplx_pass && op == PDOP_PUSH_I) {
                     if constexpr (Real<T>::cplx_pass) {
 #pragma unroll
                         for (int q = 0; q < W; ++q) O::set_const(acc[q], imag_unit<T>());
                     }
                 } else {
-                    const double c = rd_imm(dec + pc + 1);
+                    const double c = cimm;
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_const(acc[q], cvt<T>(c));
                 }
             } else if (grp == DG_CHEAP) {
                 if (op == PDOP_ADDC) {
-                    const double c = rd_imm(dec + pc + 1);
+                    const double c = cimm;
 #pragma unroll
                     for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + cvt<T>(c);
                 } else if (op == PDOP_NEG) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], from_real<T>(-1.0));
                 } else if (op == PDOP_MULC) {
-                    const double c = rd_imm(dec + pc + 1);
+                    const double c = cimm;
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], cvt<T>(c));
                 } else if (op == PDOP_ADD_X) {
@@ -291,7 +347,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                         l = reg[RSLOT ? q : 0];
                     } else {
 #pragma unroll
-                        for (int c = 0; c < NCJ; ++c) l.c[c] = src[(q * NCJ + c) * 64 + lane];
+                        for (int c = 0; c < NCJ; ++c) l.c[c] = live(c) ? src[(q * NCJ + c) * 64 + lane] : zero<T>();
                     }
                     if (op == PDOP_DIV) O::div(l, acc[q]);
                     else if (op == PDOP_SUB) O::sub(l, acc[q]);
@@ -312,18 +368,23 @@ template <class T, int K, int W, int MAXD> struct Lean {
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
                     if (op == PDOP_EXP) O::expj(acc[q]);
-                    else if (op == PDOP_POW) O::powa(acc[q], rd_imm(dec + pc + 1));
-                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], cvt<T>(rd_imm(dec + pc + 1)));
+                    else if (op == PDOP_POW) O::powa(acc[q], cimm);
+                    else if (op == PDOP_RDIVC) O::rdivc(acc[q], cvt<T>(cimm));
                     else if (op == PDOP_SQRT) O::sqrtj(acc[q]);
                     else if (op == PDOP_LOG) O::logj(acc[q]);
                     else if (op == PDOP_POWN) pown_lean(acc[q], pn);
                     else absj<K>(acc[q]);
                 }
             }
+            if constexpr (NOMIX) {
+#pragma unroll
+                for (int q = 0; q < W; ++q) acc[q].c[MIX] = zero<T>();
+            }
             if (!more) break;
             first = false;
             pc = npc;
             w = wn;
+            imm = immn;
         }
     }
 

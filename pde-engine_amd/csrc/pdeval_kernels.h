@@ -693,9 +693,12 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue(const T*
     // a jet that is exactly 0 to second order carries no information: u underflowed there
     // (exp_neg(E*exp(r**2)*..) is 0 in fp64 on most of the grid), as an analytic u that is not
     // identically 0 cannot vanish with its derivatives at a sample point
+    // (u_rx, coefficient ji(1, 1), is not in the operator -- no mixed term, kerr validator.py
+    // :77-91 -- so it is neither tested nor, in the lean grid passes, computed: kKerrMixed)
     bool allz = true;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
+        if (i == ji(1, 1)) continue;
         fin = fin && jet_coef_ok(u[i]);
         allz = allz && is_zero(u[i]);
     }

@@ -148,18 +148,40 @@ def symbolic_zero_gradient(pd, items, out) -> List[int]:
         flat = (np.all(np.isfinite(fp), axis=1) &
                 (fp.max(axis=1) - fp.min(axis=1) <= 1e-9 * np.maximum(np.abs(fp).max(axis=1), 1e-300)) &
                 np.isin(st, (CLS_ACCEPT, CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC)))
+    idx = np.flatnonzero(flat)
+    if len(idx) and all(isinstance(items[i], str) for i in idx):
+        from .hostpool import run   # strings: over the SymPy pool when it runs
+        zero = run(_zero_gradient_str, [(pd.slug, items[i]) for i in idx])
+    else:
+        zero = [_zero_gradient(pd, items[i]) for i in idx]
     rows = []
-    for i in np.flatnonzero(flat):
-        try:
-            u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
-            if u.diff(pd.x) == 0 and u.diff(pd.y) == 0:
-                st[i] = CLS_ZERO_GRADIENT
-                if 'verdict' in out:
-                    out['verdict'][i] = False
-                rows.append(i)
-        except Exception:   # noqa: BLE001  (a tree SymPy cannot differentiate keeps its class)
-            pass
+    for i, z in zip(idx.tolist(), zero):
+        if z:
+            st[i] = CLS_ZERO_GRADIENT
+            if 'verdict' in out:
+                out['verdict'][i] = False
+            rows.append(i)
     return rows
+
+
+def _zero_gradient(pd, u) -> bool:
+    """The reference's test on one candidate (tree or string); a tree SymPy cannot
+    differentiate keeps its class."""
+    try:
+        u = u if isinstance(u, sp.Basic) else pd.parse(u)
+        return bool(u.diff(pd.x) == 0 and u.diff(pd.y) == 0)
+    except Exception:   # noqa: BLE001
+        return False
+
+
+_PDS: Dict[str, object] = {}
+
+
+def _zero_gradient_str(args) -> bool:
+    slug, s = args
+    if slug not in _PDS:
+        _PDS[slug] = P.get(slug)
+    return _zero_gradient(_PDS[slug], s)
 
 
 _NONRATIONAL_OPS = {PDOP['ABS'], PDOP['SQRT'], PDOP['POW'], PDOP['LOG']}

@@ -594,11 +594,20 @@ def flatten(expr: sp.Basic, x_sym: sp.Symbol, y_sym: sp.Symbol,
 
 
 def unprovable(expr: sp.Basic) -> bool:
-    """u = exp(g)**(p/4), p > 0: SymPy keeps the power unevaluated and the reference's symbolic
-    stage (force-free validator.py:404-416) cannot reduce det to 0 (pdeval.h
-    PDEVAL_FLAG_UNPROVABLE; every such candidate of the depth-4 stream)."""
-    return (isinstance(expr, sp.Pow) and isinstance(expr.base, sp.exp) and expr.exp.is_Rational
-            and expr.exp.q == 4 and expr.exp.p > 0)
+    """u = c*exp(g)**(p/4), p > 0, c a nonzero number (1 included): SymPy keeps the power
+    unevaluated and the reference's symbolic stage (force-free validator.py:404-416) cannot
+    reduce det to 0 (pdeval.h PDEVAL_FLAG_UNPROVABLE; every such candidate of the depth-4
+    stream, the scaled forms of tests/golden/ref/ff_exp_quarter_scaled.jsonl and one of the
+    depth-5 sample)."""
+    def quarter(e):
+        return (isinstance(e, sp.Pow) and isinstance(e.base, sp.exp) and e.exp.is_Rational
+                and e.exp.q == 4 and e.exp.p > 0)
+    if quarter(expr):
+        return True
+    if isinstance(expr, sp.Mul) and len(expr.args) == 2:
+        a, b = expr.args
+        return (a.is_Number and a != 0 and quarter(b)) or (b.is_Number and b != 0 and quarter(a))
+    return False
 
 
 def program_depth(words: Sequence[int]) -> int:

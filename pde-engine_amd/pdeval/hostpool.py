@@ -64,6 +64,16 @@ def stop():
         _POOL = None
 
 
+def run(fn, items, min_items: int = 8) -> list:
+    """``[fn(x) for x in items]`` over the pool when it runs (order kept; ``fn`` a module-level
+    function of picklable arguments), else in-process.  For the per-candidate SymPy checks
+    of the host steps (pdeval.batch.symbolic_zero_gradient, the known-solution tagger)."""
+    items = list(items)
+    if _POOL is None or len(items) < min_items:
+        return [fn(x) for x in items]
+    return _POOL.map(fn, items, chunksize=max(1, len(items) // (_PROCS * 2)))
+
+
 def _compile_chunk(args):
     slug, strings = args
     from . import problem_defs as P

@@ -54,4 +54,4 @@ FLAG_COMPLEX = 1 << 16   # header flag: program pushes the imaginary unit
 FLAG_NOCOORD = 1 << 17   # header flag: program references no coordinate
 FLAG_RATIONAL = 1 << 18  # header flag: value is rational at rational points (exact det)
 FLAG_NONSMOOTH2D = 1 << 19  # header flag: contains Abs and references both coordinates
-FLAG_UNPROVABLE = 1 << 20   # header flag: u = exp(g)**(p/4), p > 0 (pdeval.h)
+FLAG_UNPROVABLE = 1 << 20   # header flag: u = c*exp(g)**(p/4), p > 0 (pdeval.h)

@@ -51,7 +51,9 @@ class KnownSolutionTagger:
         self.known = []
         self.locals = locals_
         self.rtol = rtol
+        self.slug = getattr(problem, 'slug', None)
         items = list((getattr(problem, 'known_solutions', None) or {}).items())
+        self.known_str = [k for k, _ in items]
         if not items:
             self.fps = np.zeros((0, 4))
             return
@@ -74,17 +76,16 @@ class KnownSolutionTagger:
         fp = np.asarray(fps) if fps is not None else self.fingerprints(
             [sp.sympify(u, locals=self.locals) if isinstance(u, str) else u for u in us])
         hits = self.fingerprint_hits(fp)
-        for i in np.flatnonzero(hits.any(axis=1)):
-            u = us[i]
-            for k in np.flatnonzero(hits[i]):
-                ke, name = self.known[k]
-                try:
-                    ue = sp.sympify(u, locals=self.locals) if isinstance(u, str) else u
-                    if sp.simplify(ue - ke) == 0:        # the reference's test, :1791
-                        out[i] = (True, name)
-                        break
-                except Exception:   # noqa: BLE001
-                    pass
+        pairs = [(i, k) for i in np.flatnonzero(hits.any(axis=1)).tolist()
+                 for k in np.flatnonzero(hits[i]).tolist()]
+        if self.slug and pairs and all(isinstance(us[i], str) for i, _ in pairs):
+            from .hostpool import run   # strings: the SymPy confirmations over the pool
+            same = run(_confirm_str, [(self.slug, us[i], self.known_str[k]) for i, k in pairs])
+        else:
+            same = [_confirm(us[i], self.known[k][0], self.locals) for i, k in pairs]
+        for (i, k), eq in zip(pairs, same):
+            if eq and not out[i][0]:          # the first known solution that confirms
+                out[i] = (True, self.known[k][1])
         return out
 
     def fingerprint_hits(self, fp) -> np.ndarray:
@@ -96,6 +97,30 @@ class KnownSolutionTagger:
             fin = np.isfinite(a) & np.isfinite(b)
             close = np.abs(a - b) <= 1e-12 + self.rtol * np.abs(b)
         return (fin.sum(axis=2) >= 2) & np.all(close | ~fin, axis=2)
+
+
+def _confirm(u, ke, locs) -> bool:
+    """The reference's known-solution test, ``simplify(u - known) == 0`` (:1791)."""
+    try:
+        ue = sp.sympify(u, locals=locs) if isinstance(u, str) else u
+        return bool(sp.simplify(ue - ke) == 0)
+    except Exception:   # noqa: BLE001
+        return False
+
+
+_LOCS: Dict[str, Dict[str, object]] = {}
+
+
+def _confirm_str(args) -> bool:
+    """_confirm in a pool process: the worker's sympify locals rebuilt from the problem
+    (validator_worker's, :1703-1712)."""
+    slug, u, known = args
+    if slug not in _LOCS:
+        from problems import load_problem
+        p = load_problem(slug)
+        _LOCS[slug] = {**p.unary_ops, **p.symbols, **p.constants}
+    locs = _LOCS[slug]
+    return _confirm(u, sp.sympify(known, locals=locs), locs)
 
 
 def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[str],
@@ -247,37 +272,43 @@ def _results(claimed, p, t, locs, tagger):
     return results
 
 
-def process_batches(batches, validator, kwargs, locs, tagger):
-    """process_batch over an iterable of claimed batches, pipelined: batch k+1 is compiled on
-    the host (native compiler threads, GIL released) while batch k runs on the device (its
-    own thread, GIL released in the library), and batch k-1's verdict table and tags are
-    built in between.  Yields each batch's result tuples, in order, identical to
-    process_batch's."""
+def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 2):
+    """process_batch over an iterable of claimed batches, pipelined in three stages, each on
+    its own thread: batch k+2 compiles on the host (native compiler threads; the library
+    releases the GIL), batch k+1 runs on the device (one library call, GIL released), and
+    batch k's host steps, verdict table, tags and result tuples are built on this thread.
+    ``depth`` batches are in flight at most.  Yields each batch's result tuples, in order,
+    identical to process_batch's.  An empty or None batch (the queue is idle) flushes."""
     if not (hasattr(validator, 'validate_strings') and not kwargs.get('check_regularity', False)
             and not kwargs.get('fast_point_only', False)):
         for claimed in batches:
             if claimed:
                 yield process_batch(claimed, validator, kwargs, locs, tagger)
         return
+    from collections import deque
     from concurrent.futures import ThreadPoolExecutor
     bv = validator._validator()
-    with ThreadPoolExecutor(max_workers=1) as dev:
-        inflight = None          # (claimed, prepared, future of the device result)
+
+    def run(pf):              # device thread: waits for its batch's compile, then runs it
+        p = pf.result()
+        return p, bv.run_prepared(p)
+
+    with ThreadPoolExecutor(max_workers=1) as comp, ThreadPoolExecutor(max_workers=1) as dev:
+        inflight = deque()    # (claimed, future of (prepared, device result))
+
+        def pop():
+            c0, f0 = inflight.popleft()
+            p0, r0 = f0.result()
+            return _results(c0, p0, bv.finish(p0, r0), locs, tagger)
+
         for claimed in batches:
-            if not claimed:      # idle (None) or empty: flush the batch in flight
-                if inflight is not None:
-                    c0, p0, f0 = inflight
-                    inflight = None
-                    yield _results(c0, p0, bv.finish(p0, f0.result()), locs, tagger)
+            if not claimed:
+                while inflight:
+                    yield pop()
                 continue
-            p = bv.prepare_strings([s for _, s in claimed])
-            if inflight is not None:
-                c0, p0, f0 = inflight
-                r0 = f0.result()
-                inflight = (claimed, p, dev.submit(bv.run_prepared, p))
-                yield _results(c0, p0, bv.finish(p0, r0), locs, tagger)
-            else:
-                inflight = (claimed, p, dev.submit(bv.run_prepared, p))
-        if inflight is not None:
-            c0, p0, f0 = inflight
-            yield _results(c0, p0, bv.finish(p0, f0.result()), locs, tagger)
+            pf = comp.submit(bv.prepare_strings, [s for _, s in claimed])
+            inflight.append((claimed, dev.submit(run, pf)))
+            while len(inflight) > depth:
+                yield pop()
+        while inflight:
+            yield pop()

@@ -14,6 +14,8 @@ sys.path.insert(0, os.path.join(ROOT, 'pde-engine_amd'))
 
 def main():
     import numpy as np
+    from pdeval import hostpool
+    hostpool.start()          # the SymPy pool, forked before the GPU is touched (as the worker does)
     from problems import load_problem
     from pdeval.worker import KnownSolutionTagger, filtered_kwargs, process_batches, _results
     with gzip.open(os.path.join(ROOT, 'tests', 'golden', 'streams', 'force_free_d4_validated.txt.gz'), 'rt') as f:

@@ -26,6 +26,7 @@ def stream(name, with_index=False):
 
 
 FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl', 'ff_d4_s2000.jsonl',
+          'ff_exp_quarter_scaled.jsonl',
           'ff_d4_exp_quarter.jsonl', 'ff_d4_t600.jsonl')
 # kerr_d4_range: the 243 depth-4 stream candidates whose oracle class changed with the round-3
 # rules (edge_kerr_range.txt): underflow at a reference point or on the whole grid (a pass, no
@@ -131,3 +132,13 @@ FF_COUNT_SLACK = {
     'z/(rho*(1/(-rho**2*z + z**3 + z) - 1/z) + 1 - 1/(-rho**2 + z**2 + 1))': (7, 0),
     'z/(rho/(-rho**2*z + z**3 + z) - z)': (7, 0),
 }
+
+# Depth 5 (configs[3]'s depth; the stream is not enumerable here): the reference's
+# verdicts on a seeded sample of 400 depth-5 strings of the stream's grammar
+# (gen_d5_sample.py -> streams/force_free_d5_sample.txt.gz -> ref/ff_d5_s400.jsonl).  One
+# decided row is a symbolic-stage false negative of the reference that no rule here restates:
+# u = exp(-rho/z + sqrt(rho/z)), a function of rho/z alone (det == 0), whose determinant string
+# is long enough for the reference to expand it (validator.py:407-426, "expanded det != 0")
+# and SymPy leaves sqrt(rho/z) terms un-merged.  The device accepts it (the true verdict).
+FF_D5 = ('ff_d5_s400.jsonl',)
+FF_D5_SYMBOLIC_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))'}

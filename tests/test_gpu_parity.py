@@ -460,3 +460,18 @@ def test_kerr_constants_configs(cfg):
     if kc[-1]:
         assert sum(g[0] for g in got) == 66
     assert cfg != 'a_value=0' or len(fixed) >= 3     # the host step took part
+
+
+def test_plugin_api_depth5_sample():
+    """configs[3]'s depth: the reference's verdicts and reason texts on the seeded depth-5
+    sample (golden_data.FF_D5) through the plugin on the GPU, except the one listed
+    symbolic-stage false negative of the reference."""
+    from problems import load_problem
+    import sympy as sp
+    rows = G.decided(G.ref_rows(*G.FF_D5))
+    prob = load_problem('force_free')
+    locs = {**prob.symbols, **prob.constants, **prob.unary_ops}
+    us = [sp.sympify(r['expr'], locals=locs) for r in rows]
+    got = prob.validator.validate_batch(us, check_regularity=False, fast_point_only=False)
+    bad = sorted(r['expr'] for g, r in zip(got, rows) if (g[0], g[1]) != (r['ok'], r['reason']))
+    assert bad == sorted(G.FF_D5_SYMBOLIC_DIVERGENCE), bad

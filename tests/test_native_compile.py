@@ -198,3 +198,45 @@ def test_hostpool_compile_equals_in_process():
     finally:
         hostpool.stop()
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
+
+
+def test_hostpool_host_steps_equal_in_process():
+    """The host steps' per-candidate SymPy checks over the pool (pdeval.hostpool.run): the
+    symbolic zero-gradient test and the known-solution confirmation give what they give
+    in-process."""
+    from pdeval import hostpool
+    from pdeval.batch import symbolic_zero_gradient
+    from pdeval.worker import KnownSolutionTagger, _confirm
+    from problems import load_problem
+    pd_ = P.force_free()
+    strs = ['exp(rho**2)*exp(z**2)*exp(neg(rho**2 + z**2))', 'neg(rho**2 + z**2)/(rho**2 + z**2)',
+            'rho**2', 'sqrt(rho**2)*exp(z)*exp_neg(z)', '1 + neg(rho**2 + z**2)/(rho**2 + z**2)',
+            'exp(z)*exp_neg(z)', 'rho*z/(rho*z)', 'square(exp(rho))*exp_neg(2*rho)', 'rho**2*z']
+    n = len(strs)
+
+    def fresh():
+        return {'status': np.zeros(n, dtype=np.uint8), 'verdict': np.ones(n, dtype=bool),
+                'fingerprint': np.ones((n, 4))}
+
+    a = fresh()
+    rows_in = symbolic_zero_gradient(pd_, strs, a)
+    prob = load_problem('force_free')
+    locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
+    tagger = KnownSolutionTagger.__new__(KnownSolutionTagger)
+    tagger.slug, tagger.locals = 'force_free', locs
+    tagger.known_str = ['rho**2', 'rho**2*z']
+    tagger.known = [(__import__('sympy').sympify(k, locals=locs), k) for k in tagger.known_str]
+    want = [[_confirm(s, ke, locs) for ke, _ in tagger.known] for s in strs]
+    if hostpool.start(2) is None:
+        pytest.skip('the GPU is live in this process: no fork')
+    try:
+        b = fresh()
+        rows_pool = symbolic_zero_gradient(pd_, strs, b)
+        from pdeval.worker import _confirm_str
+        got = hostpool.run(_confirm_str, [('force_free', s, k) for s in strs for k in tagger.known_str],
+                           min_items=1)
+    finally:
+        hostpool.stop()
+    assert rows_in == rows_pool and np.array_equal(a['status'], b['status'])
+    assert sum(want, []) == got
+    assert rows_in                              # the constant products are found
