@@ -481,15 +481,20 @@ extern "C" int pdeval_program_depth(const int32_t* ops, int64_t n_words) {
 
 // Algorithmic FP64 flop model per sample point (DESIGN.md "Roofline"): jet work of each
 // opcode at the problem's order plus the residual epilogue.
+// Force-free needs every coefficient of the order-4 jets (15); Kerr's operator only u, u_r,
+// u_x, u_rr, u_xx -- 5 of the 6 order-2 coefficients (no mixed term, kerr validator.py:77-91),
+// and the mixed one feeds nothing else, so it is not counted (nor computed by the lean passes).
+// Products: coefficient (i, j) of a jet product takes (i+1)(j+1) of them, so a full product is
+// 70 for K = 4 (2*70 - 15 = 125 flops) and 11 for Kerr's 5 coefficients (2*11 - 5 = 17).
 extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words) {
     const bool ff = problem_id == PDEVAL_PROBLEM_FORCE_FREE;
     const int K = ff ? 4 : 2;
-    const double NC = (K + 1) * (K + 2) / 2.0;
-    // full product: 2 * C(K+3, 3) - NC flops (K=4: 140-15 = 125; K=2: 40-6 = 34)
-    const double mulf = ff ? 125.0 : 34.0;
+    const double NC = ff ? 15.0 : 5.0;
+    const double mulf = ff ? 125.0 : 17.0;
     const double divf = mulf + NC + 10.0;
-    // Horner composition: sum over levels (2*#products) + coefficient chain
-    const double compf = ff ? (2.0 * 91.0 + 3.0 * K) : (2.0 * 11.0 + 3.0 * K);
+    // Horner composition: sum over levels (2*#products) + coefficient chain (Kerr: the level
+    // products of h (h_00 = 0) into the 5 coefficients, 6 + 2)
+    const double compf = ff ? (2.0 * 91.0 + 3.0 * K) : (2.0 * 8.0 + 3.0 * K);
     double f = 0.0;
     for (int64_t pc = 1; pc < n_words;) {
         const uint32_t op = (uint32_t)ops[pc] & 0xffu;
@@ -510,8 +515,8 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
             // coordinate powers: K+1 coefficients, then a sparse (univariate) product/quotient
             case PDOP_PUSH_P: f += 3 * (K + 1); break;
             case PDOP_ADD_P: case PDOP_SUB_P: f += 4 * (K + 1); break;
-            case PDOP_MUL_P: f += 3 * (K + 1) + (ff ? 50.0 : 14.0); break;
-            case PDOP_DIV_P: f += 3 * (K + 1) + (ff ? 60.0 : 18.0); break;
+            case PDOP_MUL_P: f += 3 * (K + 1) + (ff ? 50.0 : 11.0); break;
+            case PDOP_DIV_P: f += 3 * (K + 1) + (ff ? 60.0 : 15.0); break;
             case PDOP_RDIV_P: f += 3 * (K + 1) + divf; break;
             default: break;
         }

@@ -37,8 +37,11 @@ def _gpu_live() -> bool:
 
 
 def _init():
-    # children: SymPy only (no GPU, no threads of their own)
+    # children: SymPy only (no GPU, no threads of their own); the SymPy side is imported here,
+    # once per child, not inside the first batch that reaches it
     os.environ['OMP_NUM_THREADS'] = '1'
+    from . import problem_defs   # noqa: F401  (sympy, the flattener, the problems' locals)
+    from . import batch          # noqa: F401
 
 
 def start(procs: Optional[int] = None):

@@ -26,10 +26,24 @@ COMPILE_OK, COMPILE_DECLINED, COMPILE_PARSE = 0, 1, 2
 
 
 def _pack_text(strings: Sequence[str]) -> Tuple[bytes, np.ndarray]:
-    enc = [s.encode() for s in strings]
-    off = np.zeros(len(enc) + 1, dtype=np.int64)
-    np.cumsum([len(b) for b in enc], out=off[1:])
-    return b''.join(enc), off
+    """All strings in one buffer and their byte offsets: one join + encode, the offsets from
+    the separators' positions (a string holding the separator itself takes the slow path)."""
+    strings = list(strings)
+    off = np.zeros(len(strings) + 1, dtype=np.int64)
+    if not strings:
+        return b'', off
+    text = '\n'.join(strings).encode()
+    seps = np.flatnonzero(np.frombuffer(text, dtype=np.uint8) == 10)
+    if len(seps) != len(strings) - 1:
+        enc = [s.encode() for s in strings]
+        np.cumsum([len(b) for b in enc], out=off[1:])
+        return b''.join(enc), off
+    # string i spans [start_i, sep_i): drop the separators from the buffer's offsets
+    ends = np.append(seps, len(text))
+    starts = np.concatenate([[0], seps + 1])
+    lens = ends - starts
+    np.cumsum(lens, out=off[1:])
+    return text.replace(b'\n', b''), off
 
 
 def host_threads() -> int:

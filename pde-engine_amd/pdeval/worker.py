@@ -272,13 +272,14 @@ def _results(claimed, p, t, locs, tagger):
     return results
 
 
-def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 2):
-    """process_batch over an iterable of claimed batches, pipelined in three stages, each on
-    its own thread: batch k+2 compiles on the host (native compiler threads; the library
-    releases the GIL), batch k+1 runs on the device (one library call, GIL released), and
-    batch k's host steps, verdict table, tags and result tuples are built on this thread.
-    ``depth`` batches are in flight at most.  Yields each batch's result tuples, in order,
-    identical to process_batch's.  An empty or None batch (the queue is idle) flushes."""
+def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 3, compilers: int = 2):
+    """process_batch over an iterable of claimed batches, pipelined in three stages on their
+    own threads: the next batches compile on the host (``compilers`` threads, so that one
+    batch's native compile -- C++ threads, GIL released -- overlaps another's wait for the
+    SymPy pool), the batch before them runs on the device (one library call, GIL released),
+    and the oldest one's host steps, verdict table, tags and result tuples are built on this
+    thread.  ``depth`` batches are in flight at most.  Yields each batch's result tuples, in
+    order, identical to process_batch's.  An empty or None batch (the queue is idle) flushes."""
     if not (hasattr(validator, 'validate_strings') and not kwargs.get('check_regularity', False)
             and not kwargs.get('fast_point_only', False)):
         for claimed in batches:
@@ -293,7 +294,7 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 2):
         p = pf.result()
         return p, bv.run_prepared(p)
 
-    with ThreadPoolExecutor(max_workers=1) as comp, ThreadPoolExecutor(max_workers=1) as dev:
+    with ThreadPoolExecutor(max_workers=max(1, compilers)) as comp, ThreadPoolExecutor(max_workers=1) as dev:
         inflight = deque()    # (claimed, future of (prepared, device result))
 
         def pop():
