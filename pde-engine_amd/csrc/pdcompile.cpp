@@ -1543,7 +1543,7 @@ int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t le
         // stage then leaves terms like exp(g)**(27/2) - exp(9 g)*exp(g)**(9/2) un-merged: it
         // rejects these u although det == 0 (all 18 of the depth-4 stream: p > 0 rejected,
         // p < 0 accepted; tests/golden/ref/ff_d4_exp_quarter.jsonl), and c*exp(g)**(p/4) for a
-        // number c the same way (det is homogeneous in u; ff_exp_quarter_scaled.jsonl, and a
+        // number c the same way (det is homogeneous in u; ff_exp_power_forms.jsonl, and a
         // depth-5 sample candidate, ff_d5_s400.jsonl)
         {
             auto quarter = [&](int id) {

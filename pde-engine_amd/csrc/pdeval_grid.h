@@ -75,6 +75,9 @@ enum : uint32_t { DG_PUSH = 0, DG_CHEAP = 1, DG_POP = 2, DG_BIN = 3, DG_VAR = 4,
 #ifndef PD_KERR_NOMIX
 #define PD_KERR_NOMIX 1
 #endif
+#ifndef PD_FOLD_NEG
+#define PD_FOLD_NEG 1
+#endif
 #ifndef PD_FUSE_PUSHC
 #define PD_FUSE_PUSHC 1
 #endif
@@ -85,6 +88,38 @@ __device__ __forceinline__ uint32_t dec_group(uint64_t b) {
     if (b & kBinMask) return DG_BIN;
     if (b & kVarMask) return DG_VAR;
     return DG_OTHER;
+}
+
+// decode_kernel's sign folding, simulated: true when no folded sign reaches EXP / LOG / SQRT /
+// POW (the programs that can drop every NEG).  Malformed programs return true; the decoder
+// rejects them itself.
+__device__ __forceinline__ bool neg_fold_ok(const int32_t* prog, int plen) {
+    int sg[5] = {1, 1, 1, 1, 1};
+    int d = 0;
+    for (int pc = 1; pc < plen;) {
+        const uint32_t w = (uint32_t)prog[pc];
+        const uint32_t op = w & 0xffu;
+        if (op >= 64u) return true;
+        const uint64_t b = 1ull << op;
+        if ((kPushMask | op_bit(PDOP_PUSH_I)) & b) {
+            if (++d > 3) return true;
+            sg[d] = 1;
+        } else if (kBinMask & b) {
+            if (d < 2) return true;
+            --d;
+            const int sl = sg[d], sa = sg[d + 1];
+            if (op == PDOP_MUL || op == PDOP_DIV || op == PDOP_RDIV) sg[d] = sl * sa;
+            else if (sl == sa) sg[d] = sa;
+            else sg[d] = op == PDOP_ADD ? 1 : (op == PDOP_SUB ? sl : sa);
+        } else if (d >= 1) {
+            if (op == PDOP_NEG) sg[d] = -sg[d];
+            else if (op == PDOP_ABS || (op == PDOP_POWN && !(((w >> 8) & 0xffu) & 1u))) sg[d] = 1;
+            else if ((op == PDOP_EXP || op == PDOP_LOG || op == PDOP_SQRT || op == PDOP_POW) && sg[d] < 0)
+                return false;
+        }
+        pc += (kImmMask & b) ? ((w & PDEVAL_IMM_DD) ? 5 : 3) : 1;
+    }
+    return true;
 }
 
 template <int PROB>
@@ -99,6 +134,8 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     const uint32_t hdr = (uint32_t)prog[0];
     bool ok = plen >= 2 && (hdr & 0xffu) == 0u;   // (COMPLEX programs: the lean complex pass)
     int pc = 1, d = 0, dmax = 0, last = -1;
+    int sg[5] = {1, 1, 1, 1, 1};   // PD_FOLD_NEG: sign of the value at each stack depth (1-based)
+    const bool fold = PD_FOLD_NEG && ok && neg_fold_ok(prog, plen);
     while (ok && pc < plen) {
         const uint32_t w = (uint32_t)prog[pc];
         const uint32_t op = w & 0xffu;
@@ -140,19 +177,85 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
             const uint32_t op2 = w2 & 0xffu;
             if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || op2 == PDOP_MUL_P) {
                 dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << 21));
+                sg[d] = 1;
                 last = pc;
                 pc += len + 1;
                 continue;
             }
         }
-        dec[pc] = (int32_t)(op | (w & 0x1ff00u & ((kImmMask & b) ? 0u : ~0u)) | (dec_group(b) << 17) |
+        // Negations folded into the program (PD_FOLD_NEG): NEG flips the sign of the value
+        // at the top of the stack instead of negating 15 (Kerr: 6) coefficients, and the
+        // opcodes that follow absorb it -- s*a + c = s*(a + s*c) (ADDC with s*c; ADD_X <->
+        // SUB_X, ADD_P <-> SUB_P), products and quotients carry it (MULC, MUL_X, DIV_Y, MUL_P,
+        // RDIVC, MUL, DIV, ...: s1*s2), a sum of two signed operands picks ADD / SUB / RSUB and
+        // a sign, an even POWN or ABS clears it.  Negation is exact and every rounding is
+        // symmetric, so each coefficient is the one the program computes, up to the tracked
+        // sign.  Programs in which a folded sign would reach an opcode that needs the value
+        // itself (EXP, LOG, SQRT, POW) keep their NEGs (neg_fold_ok).  What is left at the end
+        // is bit 16 of the header word: the force-free determinant is even in u and Kerr's
+        // |L[u]| and scale are unchanged under u -> -u, so only the fingerprint (linear in u)
+        // reads it.
+        uint32_t dop = op;
+        if (fold) {
+            if (op == PDOP_NEG) {
+                const uint32_t pw = last >= 0 ? (uint32_t)dec[last] : 0u;
+                if (last >= 0 && ((pw >> 21) & 7u) + 1u <= 7u) {
+                    sg[d] = -sg[d];
+                    dec[last] = (int32_t)(pw + (1u << 21));   // the previous opcode steps over it
+                    pc += 1;
+                    continue;
+                }
+            } else if ((kPushMask | op_bit(PDOP_PUSH_I)) & b) {
+                sg[d] = 1;
+            } else if (kBinMask & b) {
+                const int sl = sg[d], sa = sg[d + 1];   // operands at depths d (lhs) and d + 1
+                if (op == PDOP_MUL || op == PDOP_DIV || op == PDOP_RDIV) {
+                    sg[d] = sl * sa;
+                } else if (sl == sa) {
+                    sg[d] = sa;                          // s*(l op a)
+                } else if (op == PDOP_ADD) {             // l - a or a - l
+                    dop = sl > 0 ? PDOP_SUB : PDOP_RSUB;
+                    sg[d] = 1;
+                } else if (op == PDOP_SUB) {             // sl*l - sa*a
+                    dop = PDOP_ADD;
+                    sg[d] = sl;
+                } else {                                 // RSUB: sa*a - sl*l
+                    dop = PDOP_ADD;
+                    sg[d] = sa;
+                }
+            } else if (sg[d] < 0) {
+                if (op == PDOP_ADDC) {
+                    const double v = -__hiloint2double(dec[pc + 2], dec[pc + 1]);
+                    dec[pc + 1] = __double2loint(v);
+                    dec[pc + 2] = __double2hiint(v);
+                } else if (op == PDOP_ADD_X) {
+                    dop = PDOP_SUB_X;
+                } else if (op == PDOP_SUB_X) {
+                    dop = PDOP_ADD_X;
+                } else if (op == PDOP_ADD_Y) {
+                    dop = PDOP_SUB_Y;
+                } else if (op == PDOP_SUB_Y) {
+                    dop = PDOP_ADD_Y;
+                } else if (op == PDOP_ADD_P) {
+                    dop = PDOP_SUB_P;
+                } else if (op == PDOP_SUB_P) {
+                    dop = PDOP_ADD_P;
+                } else if (op == PDOP_ABS || (op == PDOP_POWN && !(((w >> 8) & 0xffu) & 1u))) {
+                    sg[d] = 1;
+                } else if (op == PDOP_EXP || op == PDOP_LOG || op == PDOP_SQRT || op == PDOP_POW) {
+                    ok = false;   // (neg_fold_ok rules this out; the generic pass takes it)
+                    break;
+                }
+            }
+        }
+        dec[pc] = (int32_t)(dop | (w & 0x1ff00u & ((kImmMask & b) ? 0u : ~0u)) | (dec_group(op_bit((int)dop)) << 17) |
                             ((uint32_t)len << 21));
         last = pc;
         pc += len;
     }
     ok = ok && d == 1 && last >= 0;
     if (ok) dec[last] |= (int32_t)(1u << 20);
-    dec[0] = ok ? (int32_t)((uint32_t)dmax << 8) : (int32_t)0xff;
+    dec[0] = ok ? (int32_t)(((uint32_t)dmax << 8) | (sg[1] < 0 ? 1u << 16 : 0u)) : (int32_t)0xff;
 }
 
 // W sample points per lane (W grid rows per dispatch of one opcode): the opcode decode, the
@@ -536,9 +639,11 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     }
     // the decoded program (decode_kernel, run before pass 1): 0xff = not for the lean passes;
     // its true stack depth must fit this pass's slots
+    uint32_t u_sgn = 0u;   // a sign the decoder folded out of the program (PD_FOLD_NEG), bit 31
     if (!slow) {
         const uint32_t dh = rd_word(a.dec + beg);
         slow = (dh & 0xffu) != 0u || (int)((dh >> 8) & 0xffu) > MAXD;
+        u_sgn = (dh & 0x10000u) << 15;
     }
     if (slow) {
         if (lane == 0) list_append(slow_list, slow_count, a.list_capacity, cand);
@@ -599,7 +704,11 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {
                         const int rel = a.fp_pts[f] - base;   // uniform
-                        if (rel >= 0 && rel < 64 && lane == rel) a.out.fingerprint[cand * PDEVAL_FP_N + f] = fp_value(u[q].c[0]);
+                        if (rel >= 0 && rel < 64 && lane == rel) {
+                            const double v = fp_value(u[q].c[0]);
+                            a.out.fingerprint[cand * PDEVAL_FP_N + f] =
+                                __hiloint2double((int)((uint32_t)__double2hiint(v) ^ u_sgn), __double2loint(v));
+                        }
                     }
                 }
                 if (r.finite) {

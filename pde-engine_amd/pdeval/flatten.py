@@ -597,7 +597,7 @@ def unprovable(expr: sp.Basic) -> bool:
     """u = c*exp(g)**(p/4), p > 0, c a nonzero number (1 included): SymPy keeps the power
     unevaluated and the reference's symbolic stage (force-free validator.py:404-416) cannot
     reduce det to 0 (pdeval.h PDEVAL_FLAG_UNPROVABLE; every such candidate of the depth-4
-    stream, the scaled forms of tests/golden/ref/ff_exp_quarter_scaled.jsonl and one of the
+    stream, the scaled forms of tests/golden/ref/ff_exp_power_forms.jsonl and one of the
     depth-5 sample)."""
     def quarter(e):
         return (isinstance(e, sp.Pow) and isinstance(e.base, sp.exp) and e.exp.is_Rational

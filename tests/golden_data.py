@@ -26,7 +26,7 @@ def stream(name, with_index=False):
 
 
 FF_REF = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl', 'ff_d4_s2000.jsonl',
-          'ff_exp_quarter_scaled.jsonl',
+          'ff_exp_power_forms.jsonl',
           'ff_d4_exp_quarter.jsonl', 'ff_d4_t600.jsonl')
 # kerr_d4_range: the 243 depth-4 stream candidates whose oracle class changed with the round-3
 # rules (edge_kerr_range.txt): underflow at a reference point or on the whole grid (a pass, no
