@@ -135,7 +135,9 @@ FF_COUNT_SLACK = {
 
 # Depth 5 (configs[3]'s depth; the stream is not enumerable here): the reference's
 # verdicts on a seeded sample of 400 depth-5 strings of the stream's grammar
-# (gen_d5_sample.py -> streams/force_free_d5_sample.txt.gz -> ref/ff_d5_s400.jsonl).  One
+# (gen_d5_sample.py -> streams/force_free_d5_sample.txt.gz -> ref/ff_d5_s400.jsonl; 399 rows:
+# the reference's validate on pow_3_2(pow_neg_3_2(z**2)/(-rho**2 + z**2 + 1)) ignored its 60 s
+# alarm and was still running when the generator's 2 h limit ended it).  One
 # decided row is a symbolic-stage false negative of the reference that no rule here restates:
 # u = exp(-rho/z + sqrt(rho/z)), a function of rho/z alone (det == 0), whose determinant string
 # is long enough for the reference to expand it (validator.py:407-426, "expanded det != 0")
