@@ -614,8 +614,11 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
 // Tier B: the point stage in double-double (T = dd, or cdd for complex candidates), final,
 // one candidate per lane over a device list.  MAXD = 2: operand stack in LDS (the common
 // case); deeper or complex programs: private memory.
+#ifndef PD_DD2_WAVES
+#define PD_DD2_WAVES 2
+#endif
 template <int PROB, class T, int MAXD>
-__global__ __launch_bounds__(64, MAXD == 2 ? 2 : 1) void dd_point_kernel(KernelArgs a) {
+__global__ __launch_bounds__(64, MAXD == 2 ? PD_DD2_WAVES : 1) void dd_point_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
     constexpr int NC = nc(K);
     int64_t nwork = (int64_t)(*a.list_count);
