@@ -276,9 +276,9 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 3, co
     """process_batch over an iterable of claimed batches, pipelined in three stages on their
     own threads: the next batches compile on the host (``compilers`` threads, so that one
     batch's native compile -- C++ threads, GIL released -- overlaps another's wait for the
-    SymPy pool), the batch before them runs on the device (one library call, GIL released)
-    and through the host steps and the verdict table, and the oldest one's tags and result
-    tuples are built on this thread.  ``depth`` batches are in flight at most.  Yields each batch's result tuples, in
+    SymPy pool), the batch before them runs on the device (one library call, GIL released),
+    and the oldest one's host steps, verdict table, tags and result tuples are built on this
+    thread (host steps on the device thread measured slower: 855 k against 920-968 k/s).  ``depth`` batches are in flight at most.  Yields each batch's result tuples, in
     order, identical to process_batch's.  An empty or None batch (the queue is idle) flushes."""
     if not (hasattr(validator, 'validate_strings') and not kwargs.get('check_regularity', False)
             and not kwargs.get('fast_point_only', False)):
@@ -290,17 +290,17 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 3, co
     from concurrent.futures import ThreadPoolExecutor
     bv = validator._validator()
 
-    def run(pf):              # device thread: waits for its batch's compile, runs it, and
-        p = pf.result()       # applies the host steps (their SymPy checks wait on the pool
-        return p, bv.finish(p, bv.run_prepared(p))   # here, not on the tuple-building thread)
+    def run(pf):              # device thread: waits for its batch's compile, then runs it
+        p = pf.result()
+        return p, bv.run_prepared(p)
 
     with ThreadPoolExecutor(max_workers=max(1, compilers)) as comp, ThreadPoolExecutor(max_workers=1) as dev:
         inflight = deque()    # (claimed, future of (prepared, device result))
 
         def pop():
             c0, f0 = inflight.popleft()
-            p0, t0 = f0.result()
-            return _results(c0, p0, t0, locs, tagger)
+            p0, r0 = f0.result()
+            return _results(c0, p0, bv.finish(p0, r0), locs, tagger)
 
         for claimed in batches:
             if not claimed:
