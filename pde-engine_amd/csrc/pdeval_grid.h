@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
         if (PD_FUSE_PUSHC && PROB != PDEVAL_PROBLEM_FORCE_FREE && op == PDOP_PUSH_C && pc + len < plen) {
             const uint32_t w2 = (uint32_t)prog[pc + len];
             const uint32_t op2 = w2 & 0xffu;
-            if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || op2 == PDOP_MUL_P) {
+            if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || (PD_FUSE_PUSHC == 1 && op2 == PDOP_MUL_P)) {
                 dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << 21));
                 sg[d] = 1;
                 last = pc;
@@ -359,7 +359,8 @@ template <class T, int K, int W, int MAXD> struct Lean {
                 } else if (op == PDOP_PUSH_Y) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
-                } else if (PD_FUSE_PUSHC && K == 2 && (op == PDOP_MUL_X || op == PDOP_MUL_Y || op == PDOP_MUL_P)) {
+                } else if (PD_FUSE_PUSHC && K == 2 &&
+                           (op == PDOP_MUL_X || op == PDOP_MUL_Y || (PD_FUSE_PUSHC == 1 && op == PDOP_MUL_P))) {
                     // a fused PUSH_C c + MUL_* (decode_kernel): the two opcodes' calls
                     double pk[K + 1];
                     if (op == PDOP_MUL_P && on_y) O::pcoefs(y, pn, pk);
