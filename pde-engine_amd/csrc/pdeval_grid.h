@@ -28,9 +28,10 @@ namespace pd {
 
 // Pass 2's register operand slot (Lean::RSLOT): Kerr pass 2 21.4 -> 18.3 ms, force-free
 // 2.26 -> 2.10 ms (profiles/r03_ab1_*.log; 0 builds the variant without it).  Peephole
-// superinstructions (PUSH_C+MUL_P, any op + MULC / ADDC in one dispatch) were measured slower
-// on the same box (pass 1 83.5 vs 77.6 ms force-free, 40.6 vs 38.8 ms Kerr): the extra scalar
-// tests on every opcode cost more than the dispatches they saved; removed.
+// superinstructions tested on every opcode (PUSH_C+MUL_P, any op + MULC / ADDC in one
+// dispatch) were measured slower on the same box (pass 1 83.5 vs 77.6 ms force-free, 40.6 vs
+// 38.8 ms Kerr) and removed; the PUSH_C + MUL fusion that survives is done by the decode pass
+// into the push group (PD_FUSE_PUSHC), at no cost to other opcodes.
 #ifndef PD_LEAN_RSLOT
 #define PD_LEAN_RSLOT 1
 #endif
