@@ -362,21 +362,32 @@ template <class T, int K, int W, int MAXD> struct Lean {
                     for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
                 } else if (PD_FUSE_PUSHC && K == 2 &&
                            (op == PDOP_MUL_X || op == PDOP_MUL_Y || (PD_FUSE_PUSHC == 1 && op == PDOP_MUL_P))) {
-                    // a fused PUSH_C c + MUL_* (decode_kernel): the two opcodes' calls
+                    // a fused PUSH_C c + MUL_* (decode_kernel), in closed form: c (v + d_axis)
+                    // is (c v, c along the axis, 0 elsewhere) and c P = (c p_k along the axis).
+                    // These are the values set_const + mul_var / mul_p compute (their other
+                    // terms are products with exact zeros), without the products by zero
+                    // that the compiler may not fold (0 * v is -0 or NaN for some v) and kept
+                    // live across the loop -- which spilled 48 B per lane in round 3.
                     double pk[K + 1];
                     if (op == PDOP_MUL_P && on_y) O::pcoefs(y, pn, pk);
+                    const T c = cvt<T>(cimm);
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        O::set_const(acc[q], cvt<T>(cimm));
                         if (op == PDOP_MUL_X) {
-                            O::mul_var(acc[q], x[q], 0);
+                            O::set_const(acc[q], c * cvt<T>(x[q]));
+                            acc[q].c[ji(1, 0)] = c;
                         } else if (op == PDOP_MUL_Y) {
-                            O::mul_var(acc[q], y, 1);
+                            O::set_const(acc[q], c * cvt<T>(y));
+                            acc[q].c[ji(0, 1)] = c;
                         } else if (on_y) {
-                            O::template p_op<1>(PDOP_MUL_P, acc[q], pk);
+                            O::set_const(acc[q], c * cvt<T>(pk[0]));
+#pragma unroll
+                            for (int k = 1; k <= K; ++k) acc[q].c[ji(0, k)] = c * cvt<T>(pk[k]);
                         } else {
                             O::pcoefs(x[q], pn, pk);
-                            O::template p_op<0>(PDOP_MUL_P, acc[q], pk);
+                            O::set_const(acc[q], c * cvt<T>(pk[0]));
+#pragma unroll
+                            for (int k = 1; k <= K; ++k) acc[q].c[ji(k, 0)] = c * cvt<T>(pk[k]);
                         }
                     }
                 } else if (Real<T>::cplx_pass && op == PDOP_PUSH_I) {

@@ -23,6 +23,7 @@ numerator/denominator, which is not reproduced).
 """
 from __future__ import annotations
 
+import math
 import threading
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -213,22 +214,51 @@ def kerr_symbolic_constant(pd, items, out, ops, off) -> List[int]:
     if pd.problem_id != PROBLEM_KERR:
         return []
     st = np.asarray(out['status'])
-    rows = []
+    sel = []
     for i in np.flatnonzero(st == CLS_ZERO_GRADIENT):
         w = ops[off[i]:off[i + 1]]
         if len(w) == 0 or int(w[0]) & FLAG_NOCOORD or not _has_op(w, _NONRATIONAL_OPS):
             continue
-        try:
-            u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
-            us = sp.simplify(u)
-            if us.has(pd.x) or us.has(pd.y):
-                st[i] = CLS_REJECT_GRID
-                if 'verdict' in out:
-                    out['verdict'][i] = False
-                rows.append(i)
-        except Exception:   # noqa: BLE001  (SymPy failed: the device's class stands)
-            pass
+        sel.append(int(i))
+    if not sel:
+        return []
+    # SymPy's simplify has no time bound of its own: each check runs with one (over the SymPy
+    # pool when it runs, so the worker's pipeline does not stall); a check that hits it keeps
+    # the device's class
+    if all(isinstance(items[i], str) for i in sel):
+        from .hostpool import run
+        keeps = run(_kerr_keeps_coordinate_str, [(pd.slug, items[i]) for i in sel], min_items=1,
+                    item_timeout=KERR_SIMPLIFY_TIMEOUT_S, default=None)
+    else:
+        keeps = [_kerr_keeps_coordinate(pd, items[i]) for i in sel]
+    rows = []
+    for i, k in zip(sel, keeps):
+        if k:
+            st[i] = CLS_REJECT_GRID
+            if 'verdict' in out:
+                out['verdict'][i] = False
+            rows.append(i)
     return rows
+
+
+KERR_SIMPLIFY_TIMEOUT_S = 30.0
+
+
+def _kerr_keeps_coordinate(pd, u) -> Optional[bool]:
+    """``simplify(u).has(r) or .has(x)`` (kerr validator.py:231-240); None when SymPy fails."""
+    try:
+        u = u if isinstance(u, sp.Basic) else pd.parse(u)
+        us = sp.simplify(u)
+        return bool(us.has(pd.x) or us.has(pd.y))
+    except Exception:   # noqa: BLE001  (SymPy failed: the device's class stands)
+        return None
+
+
+def _kerr_keeps_coordinate_str(args) -> Optional[bool]:
+    slug, s = args
+    if slug not in _PDS:
+        _PDS[slug] = P.get(slug)
+    return _kerr_keeps_coordinate(_PDS[slug], s)
 
 
 def _has_prm(words) -> bool:
@@ -244,14 +274,23 @@ def _has_prm(words) -> bool:
 _KERR_REF_POINTS = ((2.5, 0.6), (7 / 3, 1 / 3), (5.0, -0.4))   # kerr validator.py:168-172
 
 
+def _fdiv(a: float, b: float) -> float:
+    """IEEE division as the device does it: x/0 is +-inf (nan for 0/0), never an exception."""
+    if b == 0.0:
+        if a != a or a == 0.0:
+            return float('nan')
+        return math.copysign(math.inf, a) * math.copysign(1.0, b)
+    return a / b
+
+
 def _exp_overflows(words, prm_values, points=_KERR_REF_POINTS) -> bool:
     """Does evaluating the program (values only, fp64, host) at a reference point take exp of
     an argument beyond the fp64 range (|arg| > 708: inf, or 0 / a subnormal that a fractional
     power or a product with an overflowed factor turns into inf or 0 * inf)?  The device's point
     stage then sees a non-finite value where the reference's arbitrary-range evaluation sees a
     finite one.  A non-real
-    intermediate (sqrt of a negative value) ends that point's evaluation without an answer."""
-    import math
+    intermediate (sqrt of a negative value) ends that point's evaluation without an answer;
+    a division by zero gives +-inf or nan, as on the device, and the evaluation goes on."""
     for x, y in points:
         st: List[float] = []
         acc = 0.0
@@ -271,26 +310,58 @@ def _exp_overflows(words, prm_values, points=_KERR_REF_POINTS) -> bool:
                 v = y if (w >> 16) & 1 else x
                 if name.startswith('PUSH'):
                     st.append(acc)
-                    acc = {'PUSH_X': x, 'PUSH_Y': y, 'PUSH_C': imm if name == 'PUSH_C' else 0.0}.get(name, v ** n)
+                    if name == 'PUSH_X':
+                        acc = x
+                    elif name == 'PUSH_Y':
+                        acc = y
+                    elif name == 'PUSH_C':
+                        acc = imm
+                    else:
+                        acc = v ** n
                 elif name in ('ADD', 'SUB', 'RSUB', 'MUL', 'DIV', 'RDIV'):
                     a = st.pop()
-                    acc = {'ADD': a + acc, 'SUB': a - acc, 'RSUB': acc - a, 'MUL': a * acc,
-                           'DIV': a / acc, 'RDIV': acc / a}[name]
+                    if name == 'ADD':
+                        acc = a + acc
+                    elif name == 'SUB':
+                        acc = a - acc
+                    elif name == 'RSUB':
+                        acc = acc - a
+                    elif name == 'MUL':
+                        acc = a * acc
+                    elif name == 'DIV':
+                        acc = _fdiv(a, acc)
+                    else:
+                        acc = _fdiv(acc, a)
                 elif name == 'ADDC':
                     acc = acc + imm
                 elif name == 'MULC':
                     acc = acc * imm
                 elif name == 'RDIVC':
-                    acc = imm / acc
+                    acc = _fdiv(imm, acc)
                 elif name == 'NEG':
                     acc = -acc
                 elif name in ('ADD_X', 'ADD_Y', 'SUB_X', 'SUB_Y', 'MUL_X', 'MUL_Y', 'DIV_X', 'DIV_Y'):
                     c = x if name.endswith('X') else y
-                    acc = {'ADD': acc + c, 'SUB': acc - c, 'MUL': acc * c, 'DIV': acc / c}[name[:3]]
+                    if name.startswith('ADD'):
+                        acc = acc + c
+                    elif name.startswith('SUB'):
+                        acc = acc - c
+                    elif name.startswith('MUL'):
+                        acc = acc * c
+                    else:
+                        acc = _fdiv(acc, c)
                 elif name in ('ADD_P', 'SUB_P', 'MUL_P', 'DIV_P', 'RDIV_P'):
                     p_ = v ** n
-                    acc = {'ADD_P': acc + p_, 'SUB_P': acc - p_, 'MUL_P': acc * p_, 'DIV_P': acc / p_,
-                           'RDIV_P': p_ / acc}[name]
+                    if name == 'ADD_P':
+                        acc = acc + p_
+                    elif name == 'SUB_P':
+                        acc = acc - p_
+                    elif name == 'MUL_P':
+                        acc = acc * p_
+                    elif name == 'DIV_P':
+                        acc = _fdiv(acc, p_)
+                    else:
+                        acc = _fdiv(p_, acc)
                 elif name == 'POWN':
                     acc = acc ** n
                 elif name == 'POW':
@@ -314,7 +385,7 @@ def _exp_overflows(words, prm_values, points=_KERR_REF_POINTS) -> bool:
 
 
 def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-10,
-                           n_grid: int = 4096, full_grid: bool = True) -> List[int]:
+                           n_grid: int = 4096, full_grid: bool = True, max_bad: int = 0) -> List[int]:
     """Kerr point rejects that only the fp64 representation caused, re-checked with the
     reference's own rule (its fast point check substitutes the values into the SYMBOLIC lhs
     and evaluates with N(., 40), kerr validator.py:163-192 -- no fp64 range, and after
@@ -331,8 +402,8 @@ def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-1
       whose program takes exp of an argument beyond +-708 at a reference point
       (_exp_overflows, a host fp64 value interpreter).
     Where the reference's rule passes, the grid stage (evaluated at the stand-ins of the
-    symbols; needs full_grid) decides: a failing point, or no finite point at all (the
-    device's rule), rejects.  Updates ``out`` in place; returns the changed rows."""
+    symbols; needs full_grid) decides: more failing points than the device's ``max_bad``, or no
+    finite point at all (the device's rule), rejects.  Updates ``out`` in place; returns the changed rows."""
     if pd.problem_id != PROBLEM_KERR or kerr is None or not full_grid:
         return []
     st = np.asarray(out['status'])
@@ -361,7 +432,7 @@ def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-1
         except Exception:   # noqa: BLE001  (the device's reject stands)
             continue
         no_grid = int(out['n_nonfinite'][i]) >= n_grid
-        st[i] = CLS_REJECT_GRID if (out['n_bad'][i] > 0 or no_grid) else CLS_ACCEPT
+        st[i] = CLS_REJECT_GRID if (out['n_bad'][i] > max_bad or no_grid) else CLS_ACCEPT
         if 'verdict' in out:
             out['verdict'][i] = st[i] == CLS_ACCEPT
         rows.append(i)
@@ -431,7 +502,8 @@ class BatchValidator:
         symbolic_zero_gradient(self.pd, items, r)
         kerr_symbolic_constant(self.pd, items, r, ops, off)
         kerr_exact_point_check(self.pd, self.kerr, items, r, ops, off, self.params.kerr_abs_tol,
-                               self.ctx.n_points - self.ctx.n_ref, bool(self.params.full_grid))
+                               self.ctx.n_points - self.ctx.n_ref, bool(self.params.full_grid),
+                               int(self.params.max_bad))
         return r
 
     def table(self, r, ops, off, notes) -> dict:

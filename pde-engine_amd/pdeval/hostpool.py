@@ -1,28 +1,47 @@
-"""Host process pool for the SymPy work the native compiler leaves (pdeval/native.py).
+"""Host process pool for the SymPy work the native compiler and the device leave to the host.
 
 The native compiler (csrc/pdcompile.cpp) compiles 99.9 % of the candidate strings on host
 threads; the few it declines go through SymPy (``sp.sympify`` + ``pdeval.flatten``, ~1.5 ms
-each), which holds the GIL.  At the rate one GPU validates, those few dominate the worker's
-host time, so they are spread over a pool of SymPy processes -- the reference parallelizes
-its SymPy validation over processes the same way (``--validators N``,
+each), which holds the GIL, and so do the host steps' per-candidate SymPy checks
+(``pdeval.batch``: the zero-gradient test, the Kerr structural constant test, the known-solution
+``simplify``).  At the rate one GPU validates, those few dominate the worker's host time, so
+they are spread over a pool of SymPy processes -- the reference parallelizes its SymPy
+validation over processes the same way (``--validators N``,
 ``general_method_paper_reproduction.py:1671-1824``).
 
 The pool is FORKED, so it must be started before the process touches the GPU (a fork of a
 process whose HIP runtime is live is not safe, and an exec from it is forbidden on the GPU
-hosts): :func:`start` refuses once torch has initialized CUDA/HIP or a libpdeval context exists,
-and :func:`compile_strings` then compiles in-process, as before.  Children never touch the GPU.
+hosts): :func:`start` refuses once torch has initialized CUDA/HIP or a libpdeval context
+exists, and the callers then run the work in-process.  For the same reason the pool is a
+FIXED set of ``fork`` children that is never replenished (``multiprocessing.Pool`` would fork a
+replacement from the parent -- by then GPU-live -- whenever a child exits): if a child dies
+(a SymPy crash, an OOM kill), the pool is marked broken and stopped, the job's missing chunks
+are computed in-process, and every later call runs in-process.  Children never touch the GPU.
+A per-item time bound (``run(..., item_timeout=s, default=d)``) is enforced inside the child
+with SIGALRM (raised as a ``BaseException`` SymPy cannot swallow); the item then yields
+``default``.
 """
 from __future__ import annotations
 
 import multiprocessing as mp
 import os
+import queue as _queue
+import signal
 import sys
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
 
 _POOL = None
-_PROCS = 0
+
+
+class _ItemTimeout(BaseException):
+    pass
+
+
+def _alarm(_sig, _frm):
+    raise _ItemTimeout()
 
 
 def _gpu_live() -> bool:
@@ -36,45 +55,170 @@ def _gpu_live() -> bool:
     return bool(lib is not None and getattr(lib, 'CONTEXTS_CREATED', 0))
 
 
-def _init():
+def _call_bounded(fn, x, item_timeout, default):
+    """fn(x), or ``default`` after ``item_timeout`` seconds (main thread only: SIGALRM)."""
+    if not item_timeout or threading.current_thread() is not threading.main_thread():
+        return fn(x)
+    old = signal.signal(signal.SIGALRM, _alarm)
+    signal.setitimer(signal.ITIMER_REAL, float(item_timeout))
+    try:
+        return fn(x)
+    except _ItemTimeout:
+        return default
+    finally:
+        signal.setitimer(signal.ITIMER_REAL, 0)
+        signal.signal(signal.SIGALRM, old)
+
+
+def _child(tasks, results):
     # children: SymPy only (no GPU, no threads of their own); the SymPy side is imported here,
     # once per child, not inside the first batch that reaches it
     os.environ['OMP_NUM_THREADS'] = '1'
+    signal.signal(signal.SIGINT, signal.SIG_IGN)
     from . import problem_defs   # noqa: F401  (sympy, the flattener, the problems' locals)
     from . import batch          # noqa: F401
+    while True:
+        msg = tasks.get()
+        if msg is None:
+            return
+        job, k, fn, items, item_timeout, default = msg
+        try:
+            out = [_call_bounded(fn, x, item_timeout, default) for x in items]
+            results.put((job, k, True, out))
+        except Exception as e:   # noqa: BLE001  (the parent recomputes the chunk in-process)
+            results.put((job, k, False, repr(e)))
 
 
-def start(procs: Optional[int] = None):
+class _FixedPool:
+    """``n`` forked SymPy processes that are never replaced.  Jobs from several threads may be
+    in flight at once: a collector thread routes each result to its job."""
+
+    def __init__(self, n: int):
+        ctx = mp.get_context('fork')
+        self.n = n
+        self.tasks = ctx.Queue()
+        self.results = ctx.Queue()
+        self.procs = [ctx.Process(target=_child, args=(self.tasks, self.results), daemon=True)
+                      for _ in range(n)]
+        for p in self.procs:
+            p.start()
+        self.broken = False
+        self.job = 0
+        self.lock = threading.Lock()
+        self.inbox = {}                      # job -> queue.Queue of (k, ok, out)
+        self._stop = False
+        self.collector = threading.Thread(target=self._collect, daemon=True)
+        self.collector.start()
+
+    def _collect(self):
+        while not self._stop:
+            try:
+                j, k, ok, out = self.results.get(timeout=0.5)
+            except _queue.Empty:
+                if not self._stop and not all(p.is_alive() for p in self.procs):
+                    self._break()
+                    return
+                continue
+            except (EOFError, OSError):
+                return
+            with self.lock:
+                box = self.inbox.get(j)
+            if box is not None:
+                box.put((k, ok, out))
+
+    def map_chunks(self, fn, chunks, item_timeout=None, default=None) -> list:
+        """Per chunk: its result list, or None where the pool could not deliver it (a child
+        died, or fn raised in the child); the caller computes those in-process."""
+        with self.lock:
+            if self.broken:
+                return [None] * len(chunks)
+            self.job += 1
+            job = self.job
+            box = self.inbox[job] = _queue.Queue()
+        try:
+            for k, ch in enumerate(chunks):
+                self.tasks.put((job, k, fn, ch, item_timeout, default))
+            got = {}
+            while len(got) < len(chunks):
+                try:
+                    k, ok, out = box.get(timeout=0.5)
+                except _queue.Empty:
+                    if self.broken:
+                        break
+                    continue
+                got[k] = out if ok else None
+            return [got.get(k) for k in range(len(chunks))]
+        finally:
+            with self.lock:
+                self.inbox.pop(job, None)
+
+    def _break(self):
+        self.broken = True
+        self.close(graceful=False)
+
+    def close(self, graceful: bool = True):
+        if graceful and not self.broken:
+            for _ in self.procs:
+                self.tasks.put(None)
+            for p in self.procs:
+                p.join(timeout=5)
+        self._stop = True
+        for p in self.procs:
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=5)
+
+
+def pool_size(local_workers: int = 1) -> int:
+    """The box's host-thread share divided among the GPU workers of this host (one SymPy pool
+    per worker), less one for the worker's own thread."""
+    from .native import host_threads
+    return max(1, host_threads() // max(1, local_workers) - 1)
+
+
+def start(procs: Optional[int] = None, local_workers: Optional[int] = None):
     """Start the pool (idempotent).  Returns it, or None when the GPU is already live in this
-    process (the caller then compiles declined strings in-process)."""
-    global _POOL, _PROCS
-    if _POOL is not None:
+    process (the callers then run their SymPy work in-process).  ``local_workers``: GPU
+    workers sharing this host (default: LOCAL_WORLD_SIZE, else 1)."""
+    global _POOL
+    if _POOL is not None and not _POOL.broken:
         return _POOL
     if _gpu_live():
         return None
-    from .native import host_threads
-    n = procs if procs is not None else max(1, host_threads() - 1)
-    _POOL = mp.get_context('fork').Pool(n, initializer=_init)
-    _PROCS = n
+    if local_workers is None:
+        local_workers = int(os.environ.get('LOCAL_WORLD_SIZE', '1') or 1)
+    n = procs if procs is not None else pool_size(local_workers)
+    _POOL = _FixedPool(n)
     return _POOL
 
 
 def stop():
     global _POOL
     if _POOL is not None:
-        _POOL.terminate()
-        _POOL.join()
+        _POOL.close()
         _POOL = None
 
 
-def run(fn, items, min_items: int = 8) -> list:
+def active() -> bool:
+    return _POOL is not None and not _POOL.broken
+
+
+def run(fn, items, min_items: int = 8, item_timeout: Optional[float] = None, default=None) -> list:
     """``[fn(x) for x in items]`` over the pool when it runs (order kept; ``fn`` a module-level
     function of picklable arguments), else in-process.  For the per-candidate SymPy checks
-    of the host steps (pdeval.batch.symbolic_zero_gradient, the known-solution tagger)."""
+    of the host steps (pdeval.batch).  ``item_timeout``: seconds per item, after which the item
+    yields ``default`` (in the pool; in-process only on the main thread)."""
     items = list(items)
-    if _POOL is None or len(items) < min_items:
-        return [fn(x) for x in items]
-    return _POOL.map(fn, items, chunksize=max(1, len(items) // (_PROCS * 2)))
+    if not active() or len(items) < min_items:
+        return [_call_bounded(fn, x, item_timeout, default) for x in items]
+    k = max(1, min(_POOL.n * 2, len(items)))
+    step = (len(items) + k - 1) // k
+    chunks = [items[i:i + step] for i in range(0, len(items), step)]
+    parts = _POOL.map_chunks(fn, chunks, item_timeout, default)
+    out: list = []
+    for ch, part in zip(chunks, parts):
+        out.extend(part if part is not None else [_call_bounded(fn, x, item_timeout, default) for x in ch])
+    return out
 
 
 def _compile_chunk(args):
@@ -89,11 +233,13 @@ def compile_strings(pd_, strings: Sequence[str]):
     in-process.  Same (ops, offsets, notes)."""
     from . import problem_defs as P
     strings = list(strings)
-    if _POOL is None or len(strings) < 8:
+    if not active() or len(strings) < 8:
         return P.compile_strings(pd_, strings)
-    k = max(1, min(_PROCS * 2, len(strings) // 4))
+    k = max(1, min(_POOL.n * 2, len(strings) // 4))
     step = (len(strings) + k - 1) // k
-    parts = _POOL.map(_compile_chunk, [(pd_.slug, strings[i:i + step]) for i in range(0, len(strings), step)])
+    args = [(pd_.slug, strings[i:i + step]) for i in range(0, len(strings), step)]
+    parts = [p[0] if p is not None else _compile_chunk(a)
+             for a, p in zip(args, _POOL.map_chunks(_compile_chunk, [[a] for a in args]))]
     ops_l: List[np.ndarray] = []
     offs = [np.zeros(1, dtype=np.int64)]
     notes: List[Optional[str]] = []

@@ -10,11 +10,14 @@ through ``torch.distributed`` (:func:`gather_verdicts`; gloo in the CPU tests).
 
 The gathered bitmap is the DEVICE's verdict, before the host steps of ``pdeval.batch``
 (``BatchValidator.host_steps``: the symbolic zero-gradient re-check, the Kerr structural
-constant re-check and the Kerr a = 0 exact point check).  Those steps only ever turn a verdict
-from True to False, and only for candidates whose device fingerprint is flat or whose class is
-ZERO_GRADIENT / a point reject; a caller that needs the plugin's exact verdicts runs them on
-its own shard's status (they need the candidate's tree) and gathers after, as
-``pdeval.worker`` does per batch.
+constant re-check and the Kerr exact point check).  Those steps change verdicts in BOTH
+directions: the zero-gradient and constant re-checks turn True into False, but the Kerr exact
+point check turns a device point reject into an accept where only fp64 range caused the reject
+(a_value = 0, exp beyond +-708 at a reference point).  So the gathered bitmap under-accepts
+such Kerr candidates relative to the plugin.  A caller that needs the plugin's verdicts runs
+the host steps on its own shard (they need the candidate strings) and gathers the re-packed
+bits after (:func:`pack_bits` of the host-stepped verdicts), as ``pdeval.worker`` does per
+batch.
 """
 from __future__ import annotations
 

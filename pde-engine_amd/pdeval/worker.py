@@ -125,11 +125,23 @@ def _confirm_str(args) -> bool:
 
 def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[str],
                      problem_name: str = 'force_free', task_queue=None, result_queue=None,
-                     batch_size: int = 4096, device: int = 0, idle_exit_s: Optional[float] = None):
-    """Worker process body (one per GPU).  Returns the number of candidates validated."""
-    from problems import load_problem
+                     batch_size: int = 4096, device: int = 0, idle_exit_s: Optional[float] = None,
+                     local_workers: Optional[int] = None):
+    """Worker process body (one per GPU).  Returns the number of candidates validated.
+    ``local_workers``: GPU workers on this host (their SymPy pools share its cores)."""
     from . import hostpool
-    hostpool.start()          # the SymPy pool for declined strings, before the GPU is touched
+    # the SymPy pool for declined strings and host checks, before the GPU is touched
+    hostpool.start(local_workers=local_workers)
+    try:
+        return _worker_loop(run_id, table_name, db_path, problem_name, task_queue, result_queue,
+                            batch_size, device, idle_exit_s)
+    finally:
+        hostpool.stop()
+
+
+def _worker_loop(run_id, table_name, db_path, problem_name, task_queue, result_queue, batch_size,
+                 device, idle_exit_s):
+    from problems import load_problem
     problem = load_problem(problem_name)
     validator = problem.validator
     if hasattr(validator, 'device'):

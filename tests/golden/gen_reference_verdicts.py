@@ -163,6 +163,7 @@ def main():
     ap.add_argument('--out', required=True)
     ap.add_argument('--depth', type=int, default=None, help='only candidates of this depth')
     ap.add_argument('--sample', type=int, default=0, help='seeded sample size (0 = all)')
+    ap.add_argument('--start', type=int, default=0, help='skip the first START input rows')
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--timeout', type=int, default=60)
     ap.add_argument('--procs', type=int, default=os.cpu_count())
@@ -210,6 +211,7 @@ def main():
     else:
         with open(a.input) as f:
             items = [(i, 0, l.strip()) for i, l in enumerate(f) if l.strip()]
+    items = items[a.start:]
     if a.depth is not None:
         items = [it for it in items if it[1] == a.depth]
     if a.sample and a.sample < len(items):
@@ -220,6 +222,8 @@ def main():
         n = 0
         for rec in pool.imap_unordered(_verdict_one, items, chunksize=1):
             rec['problem'] = a.problem
+            if a.timeout != 60:
+                rec['limit_s'] = a.timeout
             if a.problem != 'force_free' and (a.kerr_a_value != '1/10' or a.kerr_op_a_zero):
                 rec['kerr'] = {'M_value': '1', 'a_value': a.kerr_a_value, 'op_a_zero': a.kerr_op_a_zero}
             f.write(json.dumps(rec) + '\n')

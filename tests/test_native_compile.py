@@ -182,7 +182,7 @@ def test_format_reasons_equals_reason_for(prob):
     assert not bad, bad[:5]
 
 
-def test_hostpool_compile_equals_in_process():
+def _hostpool_compile_body():
     """pdeval.hostpool (the SymPy process pool for declined strings, forked before any GPU
     use) returns exactly what problem_defs.compile_strings returns in-process."""
     from pdeval import hostpool
@@ -191,8 +191,7 @@ def test_hostpool_compile_equals_in_process():
     declined = [s for s, x in zip(strs, st) if x != native.COMPILE_OK][:40]
     assert declined
     want = P.compile_strings(P.force_free(), declined)
-    if hostpool.start(2) is None:
-        pytest.skip('the GPU is live in this process: no fork')
+    assert hostpool.start(2) is not None          # a fresh process: the GPU is not live
     try:
         got = hostpool.compile_strings(P.force_free(), declined)
     finally:
@@ -200,7 +199,7 @@ def test_hostpool_compile_equals_in_process():
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[2]
 
 
-def test_hostpool_host_steps_equal_in_process():
+def _hostpool_host_steps_body():
     """The host steps' per-candidate SymPy checks over the pool (pdeval.hostpool.run): the
     symbolic zero-gradient test and the known-solution confirmation give what they give
     in-process."""
@@ -227,8 +226,7 @@ def test_hostpool_host_steps_equal_in_process():
     tagger.known_str = ['rho**2', 'rho**2*z']
     tagger.known = [(__import__('sympy').sympify(k, locals=locs), k) for k in tagger.known_str]
     want = [[_confirm(s, ke, locs) for ke, _ in tagger.known] for s in strs]
-    if hostpool.start(2) is None:
-        pytest.skip('the GPU is live in this process: no fork')
+    assert hostpool.start(2) is not None          # a fresh process: the GPU is not live
     try:
         b = fresh()
         rows_pool = symbolic_zero_gradient(pd_, strs, b)
@@ -240,3 +238,69 @@ def test_hostpool_host_steps_equal_in_process():
     assert rows_in == rows_pool and np.array_equal(a['status'], b['status'])
     assert sum(want, []) == got
     assert rows_in                              # the constant products are found
+
+
+def _in_fresh_process(fn_name):
+    """Run one of the pool bodies in a fresh interpreter: the pool forks only from a process
+    whose GPU is not live, and earlier tests of this session may have created a context."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (f"import sys; sys.path[:0] = [{here!r}, {os.path.join(os.path.dirname(here), 'pde-engine_amd')!r}]; "
+            f"import test_native_compile as t; t.{fn_name}(); print('BODY-OK')")
+    p = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0 and 'BODY-OK' in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
+
+
+def test_hostpool_compile_equals_in_process():
+    """pdeval.hostpool (the SymPy process pool for declined strings, forked before any GPU
+    use) returns exactly what problem_defs.compile_strings returns in-process."""
+    _in_fresh_process('_hostpool_compile_body')
+
+
+def test_hostpool_host_steps_equal_in_process():
+    """The host steps' per-candidate SymPy checks over the pool (pdeval.hostpool.run) give
+    what they give in-process."""
+    _in_fresh_process('_hostpool_host_steps_body')
+
+
+def _square(x):
+    return x * x
+
+
+def _slow_or_die(x):
+    import time
+    if x == 'die':
+        os._exit(3)             # a child that dies (as an OOM kill would)
+    if x == 'slow':
+        time.sleep(30)
+    return x
+
+
+def _hostpool_faults_body():
+    from pdeval import hostpool
+    assert hostpool.start(2) is not None
+    try:
+        assert hostpool.run(_square, list(range(20))) == [i * i for i in range(20)]
+        # a per-item bound: the slow item yields the default, the others their value
+        got = hostpool.run(_slow_or_die, ['a', 'slow', 'b'] * 3, min_items=1, item_timeout=1.0, default='T')
+        assert got == ['a', 'T', 'b'] * 3, got
+        # a child dies: the pool is marked broken (never re-forked), the job completes in-process
+        pids = [p.pid for p in hostpool._POOL.procs]
+        hostpool._POOL.tasks.put((-1, 0, _slow_or_die, ['die'], None, None))
+        import time
+        t0 = time.time()
+        while hostpool.active() and time.time() - t0 < 20:
+            time.sleep(0.1)
+        assert not hostpool.active()
+        assert hostpool.run(_square, list(range(10)), min_items=1) == [i * i for i in range(10)]
+        assert all(not p.is_alive() for p in hostpool._POOL.procs)
+        assert pids
+    finally:
+        hostpool.stop()
+
+
+def test_hostpool_fixed_children_timeout_and_death():
+    """The pool's children are never replaced: a dead child marks the pool broken and the
+    work runs in-process; a per-item time bound yields the default."""
+    _in_fresh_process('_hostpool_faults_body')
