@@ -425,20 +425,54 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
                                   'tuples_identical': got == ref}
     sample = random.Random(0).sample(items, min(inline_n, len(items)))
     v = prob.validator
-    t0 = time.perf_counter()
+    t_parse = t_val = 0.0
     n_ok = 0
     for _, s in sample:
-        ok, _ = v.validate(sp.sympify(s, locals=locs), **kw)
+        t0 = time.perf_counter()
+        u = sp.sympify(s, locals=locs)          # the driver's parse (:1257), before validate
+        t1 = time.perf_counter()
+        ok, _ = v.validate(u, **kw)
+        t_val += time.perf_counter() - t1
+        t_parse += t1 - t0
         n_ok += bool(ok)
-    dt = time.perf_counter() - t0
+    dt = t_parse + t_val
     out['inline_validate'] = {'sample': len(sample), 'seconds': round(dt, 3),
-                              'candidates_per_s': round(len(sample) / dt), 'valid': n_ok}
+                              'candidates_per_s': round(len(sample) / dt), 'valid': n_ok,
+                              'validate_only_per_s': round(len(sample) / t_val),
+                              'us_per_call': {'driver_sympify': round(1e6 * t_parse / len(sample), 1),
+                                              'validate': round(1e6 * t_val / len(sample), 1)},
+                              'validate_split_us': inline_split(v, sample[:500], locs)}
     # headline: the worker's default queue batch (validator_worker batch_size=4096); the
     # larger batches are detail.  Every pipelined run must give process_batch's tuples.
     out['tuples_identical_all'] = all(out[k]['tuples_identical'] for k in out if k.startswith('pipelined'))
     out['headline_batch'] = batch
     out['candidates_per_s'] = out[f'pipelined_b{batch}']['candidates_per_s'] if out['tuples_identical_all'] else None
     return out
+
+
+def inline_split(v, sample, locs):
+    """Where one validate(u) call's time goes (force-free plugin): the canonical tree, the
+    compile (flatten.py), the device call (pdeval_validate_batch: upload, launch chain or its
+    captured graph, download, sync) and the host steps + reason."""
+    import sympy as sp
+    from pdeval import problem_defs as P
+    bv = v._validator()
+    pd = P.get('force_free')
+    t = {'canon': 0.0, 'compile': 0.0, 'device': 0.0, 'host': 0.0}
+    for _, s in sample:
+        u0 = sp.sympify(s, locals=locs)
+        t0 = time.perf_counter()
+        u = v._canon(u0)
+        t1 = time.perf_counter()
+        ops, off, notes = P.compile_exprs(pd, [u])
+        t2 = time.perf_counter()
+        r = bv.run(ops, off)
+        t3 = time.perf_counter()
+        bv.table(bv.host_steps(r, ops, off, [u]), ops, off, notes)
+        t4 = time.perf_counter()
+        for k, a, b in (('canon', t0, t1), ('compile', t1, t2), ('device', t2, t3), ('host', t3, t4)):
+            t[k] += b - a
+    return {k: round(1e6 * x / len(sample), 1) for k, x in t.items()}
 
 
 def cpu_baseline_sympy(procs, budget_s):

@@ -37,6 +37,7 @@ namespace pd {
 #endif
 
 constexpr uint64_t op_bit(int op) { return 1ull << op; }
+constexpr int PTAB_N = 17;   // coordinate-power tables: 0 <= n <= 16 (the compilers emit 2 <= n <= 16)
 constexpr uint64_t kImmMask = op_bit(PDOP_PUSH_C) | op_bit(PDOP_ADDC) | op_bit(PDOP_MULC) |
                               op_bit(PDOP_RDIVC) | op_bit(PDOP_POW);
 constexpr uint64_t kPushMask = op_bit(PDOP_PUSH_X) | op_bit(PDOP_PUSH_Y) | op_bit(PDOP_PUSH_C) |
@@ -145,6 +146,11 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
         const int len = (kImmMask & b) ? ((w & PDEVAL_IMM_DD) ? 5 : 3) : 1;
         if (pc + len > plen) { ok = false; break; }
         if (op == PDOP_POWN && ((w >> 8) & 0xffu) > 8u) { ok = false; break; }   // (pown_lean)
+        // coordinate powers come from the power tables (ptab_kernel): 2 <= n < PTAB_N
+        if ((kPOpMask | op_bit(PDOP_PUSH_P)) & b) {
+            const uint32_t pn = (w >> 8) & 0xffu;
+            if (pn < 2u || pn >= (uint32_t)PTAB_N) { ok = false; break; }
+        }
         if ((kPushMask | op_bit(PDOP_PUSH_I)) & b) {
             if (++d > 3) { ok = false; break; }
             dmax = max(dmax, d);
@@ -259,6 +265,53 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     dec[0] = ok ? (int32_t)(((uint32_t)dmax << 8) | (sg[1] < 0 ? 1u << 16 : 0u)) : (int32_t)0xff;
 }
 
+// ---- coordinate-power tables.  A coordinate power v**n (PDOP_*_P) enters the interpreter as
+// the univariate jet p_k = C(n,k) v^(n-k), k <= K (JetOps::pcoefs): per opcode and grid row,
+// a loop of n - K multiplications, K + 1 more, and the binomials by division.  The values
+// depend only on (n, v), and v takes nx + ny values per context, so ptab_kernel evaluates
+// JetOps::pcoefs once for every (n, grid abscissa) and (n, grid ordinate) -- the same function,
+// so the interpreter reads bit-identical values -- and the lean passes load them:
+//   x part  [n][row][k]   wave-uniform (one grid row per W slot): scalar loads
+//   y part  [n][k][j]     lane j: one coalesced vector load per coefficient
+template <int K> constexpr size_t ptab_doubles(int nx, int ny) { return (size_t)PTAB_N * (K + 1) * (size_t)(nx + ny); }
+template <int K>
+__global__ __launch_bounds__(256) void ptab_kernel(const double* gx, const double* gy, int nx, int ny, double* tab) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nxt = (int64_t)PTAB_N * nx;
+    double pk[K + 1];
+    if (t < nxt) {
+        const int n = (int)(t / nx), i = (int)(t % nx);
+        JetOps<double, K>::pcoefs(gx[i], n, pk);
+#pragma unroll
+        for (int k = 0; k <= K; ++k) tab[((size_t)n * nx + i) * (K + 1) + k] = pk[k];
+    } else if (t < nxt + (int64_t)PTAB_N * ny) {
+        const int64_t u = t - nxt;
+        const int n = (int)(u / ny), j = (int)(u % ny);
+        JetOps<double, K>::pcoefs(gy[j], n, pk);
+        double* ty = tab + nxt * (K + 1);
+#pragma unroll
+        for (int k = 0; k <= K; ++k) ty[((size_t)n * (K + 1) + k) * ny + j] = pk[k];
+    }
+}
+// PD_PTAB (force-free) / PD_PTAB_KERR: 1 = both tables, 2 = the x table only (the lane's y
+// powers computed in place: a vector load of the y table is a dependent global-memory access
+// per opcode), 0 = none.  Force-free pass 1, same box (profiles/r04_c_*): none 150.3 ms, both
+// 151.7, x only 149.3; at 5 waves/SIMD (fewer VGPRs with the tables) x only 146.9, both 147.9,
+// none 155.5 (96 B of spill).
+#ifndef PD_PTAB
+#define PD_PTAB 2
+#endif
+#ifndef PD_PTAB_KERR
+#define PD_PTAB_KERR 2
+#endif
+// Where a lane finds its coordinate-power coefficients: x rows px[q] (wave-uniform), the
+// lane's ordinate py; strides per n: sx (x part), sy (y part), and ny between coefficients.
+template <int W> struct PowTab {
+    const double* px[W];
+    const double* py;
+    int sx, sy, ny;
+};
+
 // W sample points per lane (W grid rows per dispatch of one opcode): the opcode decode, the
 // dispatch branches and the immediate loads are paid once for W jets.  Force-free runs W = 1
 // (two 15-coefficient jets per operand would not fit 128 VGPRs); Kerr's 6-coefficient jets run
@@ -300,9 +353,30 @@ template <class T, int K, int W, int MAXD> struct Lean {
     // Evaluate a decoded program (decode_kernel; `dec` at the program's header word) at
     // (x[w], y), w < W; inv_x = 1/x, inv_y = 1/y (as rcp() forms them).  x[] is wave-uniform
     // (one grid row each), y is the lane's ordinate.
+    // coordinate-power coefficients of v**n at row slot q (x) or at the lane's ordinate (y)
+    static constexpr int PTAB = K == 4 ? PD_PTAB : PD_PTAB_KERR;
+    static __device__ __forceinline__ void pco_x(const PowTab<W>& pt, const double (&x)[W], int q, int n, double* pk) {
+        if constexpr (PTAB != 0) {
+            const double* p = pt.px[q] + (size_t)n * pt.sx;
+#pragma unroll
+            for (int k = 0; k <= K; ++k) pk[k] = rd_sf64(p + k);
+        } else {
+            O::pcoefs(x[q], n, pk);
+        }
+    }
+    static __device__ __forceinline__ void pco_y(const PowTab<W>& pt, double y, int n, double* pk) {
+        if constexpr (PTAB == 1) {
+            const double* p = pt.py + (size_t)n * pt.sy;
+#pragma unroll
+            for (int k = 0; k <= K; ++k) pk[k] = p[(size_t)k * pt.ny];
+        } else {
+            O::pcoefs(y, n, pk);
+        }
+    }
+
     static __device__ __forceinline__ void run(const int32_t* dec, const double (&x)[W], double y,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
-                                               T* stk, int lane) {
+                                               T* stk, int lane, const PowTab<W>& pt) {
         // MAXD = 3 (pass 2): the upper of the two operand slots lives in VGPRs, the lower in
         // LDS -- two LDS slots of W = 2 Kerr jets (12 KiB per wave) held pass 2 at ~3 waves
         // per SIMD; with one, VGPRs set the occupancy
@@ -347,13 +421,13 @@ template <class T, int K, int W, int MAXD> struct Lean {
                 } else if (op == PDOP_PUSH_P) {
                     double pk[K + 1];
                     if (on_y) {
-                        O::pcoefs(y, pn, pk);
+                        pco_y(pt, y, pn, pk);
 #pragma unroll
                         for (int q = 0; q < W; ++q) O::template set_p<1>(acc[q], pk);
                     } else {
 #pragma unroll
                         for (int q = 0; q < W; ++q) {
-                            O::pcoefs(x[q], pn, pk);
+                            pco_x(pt, x, q, pn, pk);
                             O::template set_p<0>(acc[q], pk);
                         }
                     }
@@ -369,7 +443,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                     // that the compiler may not fold (0 * v is -0 or NaN for some v) and kept
                     // live across the loop -- which spilled 48 B per lane in round 3.
                     double pk[K + 1];
-                    if (op == PDOP_MUL_P && on_y) O::pcoefs(y, pn, pk);
+                    if (op == PDOP_MUL_P && on_y) pco_y(pt, y, pn, pk);
                     const T c = cvt<T>(cimm);
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
@@ -384,7 +458,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
 #pragma unroll
                             for (int k = 1; k <= K; ++k) acc[q].c[ji(0, k)] = c * cvt<T>(pk[k]);
                         } else {
-                            O::pcoefs(x[q], pn, pk);
+                            pco_x(pt, x, q, pn, pk);
                             O::set_const(acc[q], c * cvt<T>(pk[0]));
 #pragma unroll
                             for (int k = 1; k <= K; ++k) acc[q].c[ji(k, 0)] = c * cvt<T>(pk[k]);
@@ -440,13 +514,13 @@ template <class T, int K, int W, int MAXD> struct Lean {
             } else if (grp == DG_POP) {
                 double pk[K + 1];
                 if (on_y) {
-                    O::pcoefs(y, pn, pk);
+                    pco_y(pt, y, pn, pk);
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::template p_op<1>(op, acc[q], pk);
                 } else {
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        O::pcoefs(x[q], pn, pk);
+                        pco_x(pt, x, q, pn, pk);
                         O::template p_op<0>(op, acc[q], pk);
                     }
                 }
@@ -582,10 +656,11 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
     }
 }
 
-// waves per SIMD of pass 1: force-free 4 (116 VGPRs; 5 waves spill 96 B/lane and measured
-// 85.6 vs 84.2 ms), Kerr 6 (80 VGPRs with the late coefficient loads; 5: 49.0 ms, 6: 46.5)
+// waves per SIMD of pass 1: force-free 5 (96 VGPRs with the x power table, 48 B of spill;
+// 4 waves 149.3 vs 146.9 ms, profiles/r04_c_*), Kerr 6 (80 VGPRs with the late coefficient
+// loads; 5: 49.0 ms, 6: 46.5)
 #ifndef PD_GRID_WAVES_PER_SIMD
-#define PD_GRID_WAVES_PER_SIMD 4
+#define PD_GRID_WAVES_PER_SIMD 5
 #endif
 #ifndef PD_KERR_WAVES_PER_SIMD
 #define PD_KERR_WAVES_PER_SIMD 6
@@ -683,8 +758,15 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             x[q] = rd_sf64(a.gx + min(row + q, a.nx - 1));   // a tail row past nx: unused
             inv_x[q] = rd_sf64(a.gx + a.nx + min(row + q, a.nx - 1));   // = rcp(x[q]), host table
         }
+        PowTab<W> pt;
+        pt.sx = a.nx * (K + 1);
+        pt.sy = (K + 1) * a.ny;
+        pt.ny = a.ny;
+#pragma unroll
+        for (int q = 0; q < W; ++q) pt.px[q] = a.ptab + (size_t)min(row + q, a.nx - 1) * (K + 1);
         for (int sl = 0; sl < per_row; ++sl) {
             const double y = per_row == 1 ? y0 : a.gy[sl * 64 + lane];
+            pt.py = a.ptab + (size_t)PTAB_N * a.nx * (K + 1) + sl * 64 + lane;
             const double inv_y = per_row == 1 ? inv_y0 : rcp(y);
             // Kerr: this point's operator coefficients (a 128 KiB table, L2-resident) are loaded
             // before the program runs, so their latency hides under the interpreter
@@ -703,7 +785,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             constexpr bool kv_late = W > 2 || (MAXD == 2 && PD_KV_LATE) || (MAXD > 2 && PD_KV_LATE_DEEP);
             if constexpr (!kv_late) load_kv();
             J u[W];
-            L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane);
+            L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane, pt);
             if constexpr (kv_late) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {

@@ -18,6 +18,18 @@ void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                            (grid_lds<PDEVAL_PROBLEM_KERR, 2>(PD_GRID_WPB)), s, a, slow_list, slow_count);
 }
 
+size_t ptab_bytes(int problem, int nx, int ny) {
+    return sizeof(double) * (problem == PDEVAL_PROBLEM_FORCE_FREE ? ptab_doubles<4>(nx, ny) : ptab_doubles<2>(nx, ny));
+}
+
+void launch_ptab(int problem, const double* gx, const double* gy, int nx, int ny, double* tab, hipStream_t s) {
+    const unsigned blocks = (unsigned)(((int64_t)PTAB_N * (nx + ny) + 255) / 256);
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE)
+        hipLaunchKernelGGL((ptab_kernel<4>), dim3(blocks), dim3(256), 0, s, gx, gy, nx, ny, tab);
+    else
+        hipLaunchKernelGGL((ptab_kernel<2>), dim3(blocks), dim3(256), 0, s, gx, gy, nx, ny, tab);
+}
+
 void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a) {
     const unsigned blocks = (unsigned)((n + 255) / 256);
     if (problem == PDEVAL_PROBLEM_FORCE_FREE)

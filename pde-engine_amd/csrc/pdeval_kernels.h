@@ -54,6 +54,10 @@ struct KernelArgs {
     const double* gy;           // ny grid ordinates (ny % 64 == 0)
     int nx, ny;
     const double* kc;           // Kerr: 4 operator coefficients per point (NULL for FF)
+    // coordinate-power tables of the lean grid passes (pdeval_grid.h ptab_kernel, built once per
+    // context), or NULL: the jets C(n,k) v^(n-k), k <= K, of v**n for 0 <= n <= 16 at every
+    // grid abscissa ([n][row][k], wave-uniform) and ordinate ([n][k][j], lane j)
+    const double* ptab;
     int n_ref;
     int n_pts;                  // n_ref + nx * ny
     int fp_pts[PDEVAL_FP_N];    // point indices whose u value is the fingerprint

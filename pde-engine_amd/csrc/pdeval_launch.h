@@ -18,6 +18,10 @@ void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a
                        int plen, double* out, uint8_t* state);
 // the lean grid passes (pdeval_grid.hip): pass 1 over all n candidates (one wave each, stack
 // <= 2), pass 2 persistent over the stack-3 list a.list (64-thread blocks)
+// the lean passes' coordinate-power tables (pdeval_grid.h ptab_kernel): size, and the build
+// from the grid abscissae / ordinates of a context (once, at creation)
+size_t ptab_bytes(int problem, int nx, int ny);
+void launch_ptab(int problem, const double* gx, const double* gy, int nx, int ny, double* tab, hipStream_t s);
 // decode every program for the lean passes (pdeval_grid.h decode_kernel) into a.dec
 void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a);
 void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,

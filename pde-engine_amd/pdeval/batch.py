@@ -49,6 +49,7 @@ class Verdict:
     n_bad: int
     n_nonfinite: int
     fingerprint: Tuple[float, ...]
+    evidence: Optional[dict] = None   # Kerr, symbolic 'text' / 'replay': the reference's last_evidence()
 
 
 def _fmt_point(v: float) -> str:
@@ -465,16 +466,129 @@ def _kerr_fast_point_check(pd, kerr, u, abs_tol) -> bool:
     return n_ok > 0 and worst < abs_tol
 
 
-class BatchValidator:
-    """One problem on one GPU.  Thread-safe (calls are serialized per context)."""
+SYMBOLIC_MODES = ('off', 'text', 'replay')
+SYMBOLIC_TIMEOUT_S = 60.0    # per candidate: the limit the reference fixtures were made with
 
-    def __init__(self, problem: str = 'force_free', device: int = 0, params=None, kerr=None):
+
+def symbolic_stage(pd, items, out, mode: str = 'text', timeout: float = SYMBOLIC_TIMEOUT_S,
+                   kerr=None) -> List[int]:
+    """Force-free: the reference's symbolic stage replayed on the host (pdeval.symbolic) where
+    it decides the verdict or the text (``problems/force_free/validator.py:404-427``):
+
+    * ``text``   -- grid rejects: SymPy's det_M and its printed length choose between "Invalid
+      (Lean could not simplify det to 0 symbolically)" and "Invalid (expanded det != 0)";
+    * ``replay`` -- also every candidate the grid found zero (ACCEPT, REJECT_SYMBOLIC): the
+      reference's symbolic verdict and text replace the device's (its false negatives, e.g. an
+      expanded det that keeps sqrt(rho/z) and rho/z apart, become rejects).
+
+    Kerr (``_kerr_symbolic_stage``): the reference's reject texts with their 240-character
+    symbolic residual, and its ``last_evidence()`` dict for the candidates that pass the point
+    stage; ``replay`` also takes the reference's exact-zero verdict.
+
+    Each candidate runs with a time bound (over the SymPy pool when items are strings); one that
+    hits it keeps the device's verdict and text.  Updates ``out`` in place (``status``,
+    ``verdict``, ``reason_override``: row -> text, and for Kerr ``evidence``: row -> dict);
+    returns the changed rows."""
+    if mode not in SYMBOLIC_MODES:
+        raise ValueError(f'symbolic mode {mode!r}: one of {SYMBOLIC_MODES}')
+    if mode == 'off':
+        return []
+    if pd.problem_id == PROBLEM_KERR:
+        return _kerr_symbolic_stage(pd, items, out, mode, timeout, kerr)
+    if pd.problem_id != PROBLEM_FORCE_FREE:
+        return []
+    st = np.asarray(out['status'])
+    cls = (CLS_REJECT_GRID,) if mode == 'text' else (CLS_REJECT_GRID, CLS_ACCEPT, CLS_REJECT_SYMBOLIC)
+    sel = np.flatnonzero(np.isin(st, cls)).tolist()
+    if not sel:
+        return []
+    from . import symbolic as S
+    args = [(pd.slug, items[i] if isinstance(items[i], str) else None, int(st[i]) != CLS_REJECT_GRID) for i in sel]
+    if all(a[1] is not None for a in args):
+        from .hostpool import run
+        res = run(S.replay_str, args, min_items=1, item_timeout=timeout, default=None)
+    else:
+        from .hostpool import _call_bounded
+        res = [_call_bounded(lambda it: S.ff_replay(it[0], pd.x, pd.y, it[1]),
+                             (items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i]),
+                              int(st[i]) != CLS_REJECT_GRID), timeout, None) for i in sel]
+    ov = out.setdefault('reason_override', {})
+    rows = []
+    for i, r in zip(sel, res):
+        if r is None:
+            continue
+        ok, text = r
+        new = CLS_ACCEPT if ok else (CLS_REJECT_GRID if st[i] == CLS_REJECT_GRID else CLS_REJECT_SYMBOLIC)
+        ov[i] = text
+        if new != st[i]:
+            st[i] = new
+            if 'verdict' in out:
+                out['verdict'][i] = bool(ok)
+        rows.append(i)
+    return rows
+
+
+def kerr_operator_spec(pd, kerr) -> Tuple[str, str, str, str]:
+    """(M, a) of the Kerr operator -- the problem's symbols, or the numbers a validator was
+    built with -- and the values its fast point check substitutes, as strings."""
+    Mv = str(sp.Rational(kerr.M_num, kerr.M_den))
+    av = str(sp.Rational(kerr.a_num, kerr.a_den))
+    return (Mv if kerr.op_M_fixed else 'M', av if kerr.op_a_fixed else 'a', Mv, av)
+
+
+def _kerr_symbolic_stage(pd, items, out, mode, timeout, kerr) -> List[int]:
+    from . import symbolic as S
+    if kerr is None:
+        from ._lib import default_kerr_constants
+        kerr = default_kerr_constants()
+    spec = kerr_operator_spec(pd, kerr)
+    st = np.asarray(out['status'])
+    code = {CLS_REJECT_POINT: 1, CLS_REJECT_GRID: 2, CLS_ACCEPT: 0}
+    sel = [i for i in range(len(st)) if int(st[i]) in code]
+    if not sel:
+        return []
+    strs = [items[i] if isinstance(items[i], str) else str(items[i]) for i in sel]
+    args = [(s_, code[int(st[i])], spec) for s_, i in zip(strs, sel)]
+    from .hostpool import run
+    res = run(S.kerr_text, args, min_items=1, item_timeout=timeout, default=None)
+    ov = out.setdefault('reason_override', {})
+    evid = out.setdefault('evidence', {})
+    rows = []
+    for i, r in zip(sel, res):
+        if r is None:
+            continue
+        text, ev, zero = r
+        if ev is not None:
+            evid[i] = ev
+        if mode == 'replay' and int(st[i]) == CLS_ACCEPT and zero is False:
+            st[i] = CLS_REJECT_GRID
+            if 'verdict' in out:
+                out['verdict'][i] = False
+        if text is not None and int(st[i]) != CLS_ACCEPT:
+            ov[i] = text
+        rows.append(i)
+    return rows
+
+
+class BatchValidator:
+    """One problem on one GPU.  Thread-safe (calls are serialized per context).
+
+    ``symbolic``: the host replay of the reference's symbolic stage (``symbolic_stage``):
+    'off' (the device's verdicts and texts), 'text' (grid rejects get the reference's branch
+    text) or 'replay' (the reference's symbolic verdicts too)."""
+
+    def __init__(self, problem: str = 'force_free', device: int = 0, params=None, kerr=None,
+                 symbolic: str = 'off', symbolic_timeout: float = SYMBOLIC_TIMEOUT_S):
         from ._lib import Context, default_params, default_kerr_constants
         self.pd = P.get(problem)
         self.device = device
         self.kerr = kerr if kerr is not None or self.pd.problem_id != PROBLEM_KERR else default_kerr_constants()
         self.ctx = Context(self.pd.problem_id, device=device, kerr=kerr)
         self.params = params if params is not None else default_params(self.pd.problem_id)
+        if symbolic not in SYMBOLIC_MODES:
+            raise ValueError(f'symbolic mode {symbolic!r}: one of {SYMBOLIC_MODES}')
+        self.symbolic = symbolic
+        self.symbolic_timeout = symbolic_timeout
         self._lock = threading.Lock()
 
     @property
@@ -488,22 +602,29 @@ class BatchValidator:
         with self._lock:
             return self.ctx.validate(ops, offsets, self.params)
 
-    def validate_exprs(self, exprs: Sequence[sp.Basic]) -> List[Verdict]:
+    def validate_exprs(self, exprs: Sequence[sp.Basic], symbolic: Optional[str] = None,
+                       symbolic_timeout: Optional[float] = None) -> List[Verdict]:
         if not exprs:
             return []
         ops, off, notes = self.compile(exprs)
-        return self._verdicts(ops, off, notes, exprs)
+        return self._verdicts(ops, off, notes, exprs, symbolic, symbolic_timeout)
 
-    def host_steps(self, r, ops, off, items):
+    def host_steps(self, r, ops, off, items, symbolic: Optional[str] = None,
+                   symbolic_timeout: Optional[float] = None):
         """The host steps every device result goes through (in place): the symbolic
         zero-gradient re-check (force-free), the structural constant re-check of numeric
-        constants with an Abs or fractional power (Kerr) and, for Kerr at a = 0, the
-        reference's exact point check."""
+        constants with an Abs or fractional power (Kerr), the reference's exact point check
+        for Kerr values beyond the fp64 range, and (force-free, ``symbolic`` != 'off') the
+        replay of the reference's symbolic stage."""
         symbolic_zero_gradient(self.pd, items, r)
         kerr_symbolic_constant(self.pd, items, r, ops, off)
         kerr_exact_point_check(self.pd, self.kerr, items, r, ops, off, self.params.kerr_abs_tol,
                                self.ctx.n_points - self.ctx.n_ref, bool(self.params.full_grid),
                                int(self.params.max_bad))
+        mode = self.symbolic if symbolic is None else symbolic
+        if mode != 'off' and (self.params.full_grid or self.problem_id == PROBLEM_KERR):
+            symbolic_stage(self.pd, items, r, mode,
+                           self.symbolic_timeout if symbolic_timeout is None else symbolic_timeout, self.kerr)
         return r
 
     def table(self, r, ops, off, notes) -> dict:
@@ -512,17 +633,21 @@ class BatchValidator:
         st = np.asarray(r['status'])
         reasons = format_reasons(self.problem_id, st, r['res_ref'], r['q_ref'], r['q_grid'],
                                  rational_flags(ops, off), notes)
+        for i, text in r.get('reason_override', {}).items():
+            reasons[i] = text
         return {**r, 'ok': st == CLS_ACCEPT, 'reasons': reasons}
 
-    def _verdicts(self, ops, off, notes, items) -> List[Verdict]:
-        r = self.host_steps(self.run(ops, off), ops, off, items)
+    def _verdicts(self, ops, off, notes, items, symbolic: Optional[str] = None,
+                  symbolic_timeout: Optional[float] = None) -> List[Verdict]:
+        r = self.host_steps(self.run(ops, off), ops, off, items, symbolic, symbolic_timeout)
         t = self.table(r, ops, off, notes)
         ok, reasons = t['ok'].tolist(), t['reasons']
         st, qr, qg = r['status'].tolist(), r['q_ref'].tolist(), r['q_grid'].tolist()
         rr, fp = r['res_ref'].tolist(), r['fingerprint'].tolist()
         nb, nn = r['n_bad'].tolist(), r['n_nonfinite'].tolist()
-        return [Verdict(ok[i], reasons[i], st[i], qr[i], tuple(rr[i]), qg[i], nb[i], nn[i], tuple(fp[i]))
-                for i in range(len(st))]
+        ev = r.get('evidence', {})
+        return [Verdict(ok[i], reasons[i], st[i], qr[i], tuple(rr[i]), qg[i], nb[i], nn[i], tuple(fp[i]),
+                        ev.get(i)) for i in range(len(st))]
 
     # ---- the worker's fast path in three phases (pdeval/worker.py pipelines them):
     # prepare (host threads, GIL released in the native compiler), run (one device call,
@@ -537,11 +662,12 @@ class BatchValidator:
     def run_prepared(self, p: dict):
         return self.run(p['ops'], p['off'])
 
-    def finish(self, p: dict, r) -> dict:
-        r = self.host_steps(r, p['ops'], p['off'], p['strings'])
+    def finish(self, p: dict, r, symbolic: Optional[str] = None, symbolic_timeout: Optional[float] = None) -> dict:
+        r = self.host_steps(r, p['ops'], p['off'], p['strings'], symbolic, symbolic_timeout)
         return self.table(r, p['ops'], p['off'], p['notes'])
 
-    def validate_strings(self, strings: Sequence[str], stats: Optional[dict] = None) -> List[Verdict]:
+    def validate_strings(self, strings: Sequence[str], stats: Optional[dict] = None,
+                         symbolic: Optional[str] = None, symbolic_timeout: Optional[float] = None) -> List[Verdict]:
         """Candidate strings in: compiled by the native compiler (csrc/pdcompile.cpp), SymPy
         only for the strings it declines (pdeval/native.py); unparsable strings get the
         UNSUPPORTED stub and an "Error: ..." reason, as on the SymPy path.  ``stats`` receives
@@ -550,7 +676,7 @@ class BatchValidator:
             return []
         from .native import compile_strings
         ops, off, notes = compile_strings(self.pd, list(strings), stats=stats)
-        return self._verdicts(ops, off, notes, list(strings))
+        return self._verdicts(ops, off, notes, list(strings), symbolic, symbolic_timeout)
 
     def close(self):
         self.ctx.close()
@@ -562,7 +688,7 @@ _VLOCK = threading.Lock()
 
 def get_validator(problem: str, device: int = 0, kerr=None) -> BatchValidator:
     """Process-wide BatchValidator per (problem, device, Kerr constants): one libpdeval context
-    per GPU and parameter set."""
+    per GPU and parameter set.  (The symbolic host mode is chosen per call by the plugins.)"""
     key = (P.get(problem).slug, device, kerr.key() if kerr is not None else None)
     with _VLOCK:
         if key not in _VALIDATORS:

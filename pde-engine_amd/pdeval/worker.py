@@ -248,7 +248,13 @@ def _process_batch_strings(claimed, validator, locs, tagger):
     reference's simplify(u - known) == 0, :1785-1798)."""
     bv = validator._validator()
     p = bv.prepare_strings([s for _, s in claimed])
-    return _results(claimed, p, bv.finish(p, bv.run_prepared(p)), locs, tagger)
+    return _results(claimed, p, bv.finish(p, bv.run_prepared(p), **_symbolic_args(validator)), locs, tagger)
+
+
+def _symbolic_args(validator) -> dict:
+    """The plugin's host replay of the reference's symbolic stage (pdeval.batch.symbolic_stage)."""
+    fn = getattr(validator, 'symbolic_args', None)
+    return fn() if fn is not None else {}
 
 
 def _results(claimed, p, t, locs, tagger):
@@ -301,6 +307,7 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 3, co
     from collections import deque
     from concurrent.futures import ThreadPoolExecutor
     bv = validator._validator()
+    sym = _symbolic_args(validator)
 
     def run(pf):              # device thread: waits for its batch's compile, then runs it
         p = pf.result()
@@ -312,7 +319,7 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 3, co
         def pop():
             c0, f0 = inflight.popleft()
             p0, r0 = f0.result()
-            return _results(c0, p0, bv.finish(p0, r0), locs, tagger)
+            return _results(c0, p0, bv.finish(p0, r0, **sym), locs, tagger)
 
         for claimed in batches:
             if not claimed:

@@ -12,10 +12,19 @@ Differences, all deliberate:
   §4); an in-memory memo keyed by ``str(u)`` is kept instead;
 * ``fast_point_only=True`` returns the point-stage verdict ("Valid foliation (point check = 0)")
   -- the reference's fast branch fails on its own symbolic stand-ins (``:298-303, :323``);
-* ``Omega`` must be 0 (the problem path, ``problems/__init__.py:83``).
+* ``Omega`` must be 0 (the problem path, ``problems/__init__.py:83``);
+* ``symbolic`` chooses how much of the reference's symbolic stage (``:404-427``) is replayed
+  on the host in SymPy (``pdeval.symbolic``): ``'off'`` (default: the device's verdicts, and
+  the Lean text for every grid reject), ``'text'`` (grid rejects get the reference's branch
+  text, "Invalid (expanded det != 0)" when SymPy's det_M prints to 3,000 characters or more)
+  or ``'replay'`` (also the reference's symbolic verdict for every candidate the grid finds
+  zero: its false negatives become rejects).  Each replayed candidate is bounded by
+  ``symbolic_timeout`` seconds and keeps the device's verdict past it.  The env var
+  ``PDEVAL_SYMBOLIC`` sets the default.
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import sympy as sp
@@ -23,16 +32,21 @@ import sympy as sp
 
 class PreciseFoliationValidator:
     def __init__(self, cache_db: Optional[str] = None, use_lean: bool = True, Omega: Any = 0,
-                 device: int = 0):
+                 device: int = 0, symbolic: Optional[str] = None, symbolic_timeout: float = 60.0):
         if Omega != 0:
             raise NotImplementedError('only the non-rotating constraint (Omega = 0) is implemented')
+        from pdeval.batch import SYMBOLIC_MODES
+        self.symbolic = symbolic or os.environ.get('PDEVAL_SYMBOLIC', 'off')
+        if self.symbolic not in SYMBOLIC_MODES:
+            raise ValueError(f'symbolic mode {self.symbolic!r}: one of {SYMBOLIC_MODES}')
+        self.symbolic_timeout = symbolic_timeout
         self.rho = sp.Symbol('rho', real=True, positive=True)
         self.z = sp.Symbol('z', real=True)
         self.Omega = Omega
         self.use_lean = use_lean
         self.cache_db = cache_db
         self.device = device
-        self._memo: Dict[Tuple[str, bool, bool], Tuple[bool, str]] = {}
+        self._memo: Dict[Tuple[sp.Basic, bool, bool, str], Tuple[bool, str]] = {}
         self._bv = None
 
     # the GPU context is created on first use (one per process and device)
@@ -43,9 +57,11 @@ class PreciseFoliationValidator:
         return self._bv
 
     def _canon(self, u: sp.Basic) -> sp.Basic:
-        # rename free symbols called rho / z to the validator's symbols (validator.py:283-284)
+        # rename free symbols called rho / z to the validator's symbols (validator.py:283-284);
+        # the driver's trees already hold them (problems/__init__.py:70-71): no substitution
         sub = {s: (self.rho if s.name == 'rho' else self.z)
                for s in u.free_symbols if getattr(s, 'name', '') in ('rho', 'z')}
+        sub = {k: v for k, v in sub.items() if k is not v}
         return u.subs(sub) if sub else u
 
     def validate(self, u: sp.Basic, check_regularity: bool = True,
@@ -59,7 +75,9 @@ class PreciseFoliationValidator:
         for i, u0 in enumerate(us):
             try:
                 u = self._canon(sp.sympify(u0))
-                key = (str(u), bool(check_regularity), bool(fast_point_only))
+                # (the tree itself is the memo key: structural equality, and its hash is cached;
+                # str(u) cost a fifth of a one-candidate call)
+                key = (u, bool(check_regularity), bool(fast_point_only), self.symbolic)
                 if key in self._memo:
                     out[i] = self._memo[key]
                     continue
@@ -79,11 +97,11 @@ class PreciseFoliationValidator:
                 prm.full_grid = 0
                 saved, bv.params = bv.params, prm
                 try:
-                    res = bv.validate_exprs([u for _, u in todo])
+                    res = bv.validate_exprs([u for _, u in todo], symbolic='off')
                 finally:
                     bv.params = saved
             else:
-                res = bv.validate_exprs([u for _, u in todo])
+                res = self._symbolic_call(bv.validate_exprs, [u for _, u in todo])
             for (key, _), i, v in zip(todo, idx, res):
                 r = (v.ok, v.reason)
                 if fast_point_only and v.cls in (0, 2, 7):   # passed the point stage
@@ -96,8 +114,15 @@ class PreciseFoliationValidator:
         validate them without building SymPy trees (native compiler, SymPy only for the
         strings it declines), with the driver's kwargs check_regularity=False,
         fast_point_only=False.  Same (bool, reason) as validate_batch(sympify(s))."""
-        res = self._validator().validate_strings(list(strings))
+        res = self._symbolic_call(self._validator().validate_strings, list(strings))
         return [(v.ok, v.reason) for v in res]
+
+    def _symbolic_call(self, fn, items):
+        return fn(items, symbolic=self.symbolic, symbolic_timeout=self.symbolic_timeout)
+
+    def symbolic_args(self) -> Dict[str, Any]:
+        """The host-replay mode of this validator, as BatchValidator.finish takes it (worker)."""
+        return {'symbolic': self.symbolic, 'symbolic_timeout': self.symbolic_timeout}
 
     def validate_known_solutions(self) -> Dict[str, bool]:
         rho, z = self.rho, self.z

@@ -17,6 +17,15 @@ in its operator everywhere; ``u``'s own symbol is then free.
 With ``defer_heavy_checks=False`` the reference's heavy checks on exact zeros (constancy,
 finiteness, axis/horizon regularity, a -> 0 monopole anchor, ``:325-342``) run on the host in
 SymPy -- only for the (rare) candidates the GPU accepts.
+
+``symbolic`` (constructor; env ``PDEVAL_SYMBOLIC``): ``'off'`` (default) gives class-level
+reject texts (a numeric residual after "residual:") and a device evidence dict; ``'text'``
+reproduces the reference's texts -- the 240-character ``numer/denom`` repr of the symbolic
+residual (``_short_residual_repr`` :249-261) -- and its ``last_evidence()`` dict
+``{lhs_string, lean_normalized, sympy_simplified_is_zero, params}`` (:296-306), which like the
+reference's is the one of the last candidate that passed the fast point check (point rejects
+leave it as it was); ``'replay'`` also takes the reference's exact-zero verdict.  Those modes
+run SymPy per candidate on the host (``pdeval.symbolic``), each bounded by ``symbolic_timeout``.
 """
 from __future__ import annotations
 
@@ -31,7 +40,14 @@ class KerrMagnetosphereValidator:
                  use_lean: bool = True, lean_det_str_max_len: int = 12000,
                  require_monopole_extension: bool = True, monopole_target: str = '1-x',
                  allow_normalization: bool = False, strict_sympy_check: bool = True,
-                 exclude_constants: bool = True, device: int = 0) -> None:
+                 exclude_constants: bool = True, device: int = 0, symbolic: Optional[str] = None,
+                 symbolic_timeout: float = 60.0) -> None:
+        import os
+        from pdeval.batch import SYMBOLIC_MODES
+        self.symbolic = symbolic or os.environ.get('PDEVAL_SYMBOLIC', 'off')
+        if self.symbolic not in SYMBOLIC_MODES:
+            raise ValueError(f'symbolic mode {self.symbolic!r}: one of {SYMBOLIC_MODES}')
+        self.symbolic_timeout = symbolic_timeout
         self._kerr = self.device_constants(M, a, M_value, a_value)
         self.r, self.x, self.M, self.a = r, x, M, a
         self.M_value, self.a_value = M_value, a_value
@@ -88,6 +104,10 @@ class KerrMagnetosphereValidator:
     def last_evidence(self) -> Dict[str, Any]:
         return self._last_evidence
 
+    def symbolic_args(self) -> Dict[str, Any]:
+        """The host-text mode of this validator, as BatchValidator.finish takes it (worker)."""
+        return {'symbolic': self.symbolic, 'symbolic_timeout': self.symbolic_timeout}
+
     # --------------------------------------------------------------- validation
     def validate(self, u: sp.Basic, check_regularity: bool = True, fast_point_only: bool = False,
                  *, lean_first: bool = True, defer_heavy_checks: bool = True,
@@ -114,14 +134,19 @@ class KerrMagnetosphereValidator:
             except Exception as e:  # noqa: BLE001
                 out[i] = (False, f'Validation error: {e}')
         if exprs:
-            res = self._validator().validate_exprs(exprs)
+            res = self._validator().validate_exprs(exprs, symbolic=self.symbolic,
+                                                   symbolic_timeout=self.symbolic_timeout)
             for u, i, v in zip(exprs, idx, res):
                 ok, reason = v.ok, v.reason
-                self._last_evidence = {
-                    'kernel_class': v.cls, 'max_abs_lhs_at_test_points': v.q_ref,
-                    'max_scaled_lhs_on_grid': v.q_grid,
-                    'params': {'M': str(self.M_value), 'a': str(self.a_value)},
-                }
+                if self.symbolic == 'off':
+                    self._last_evidence = {
+                        'kernel_class': v.cls, 'max_abs_lhs_at_test_points': v.q_ref,
+                        'max_scaled_lhs_on_grid': v.q_grid,
+                        'params': {'M': str(self.M_value), 'a': str(self.a_value)},
+                    }
+                elif v.evidence is not None:
+                    # the reference records evidence only past its fast point check (:296-306)
+                    self._last_evidence = v.evidence
                 # the reference consults its cache only after the fast point check passed and
                 # writes False only when the exact-zero stage failed (:274-281, :308-315): a
                 # repeated point reject is re-checked (same reason), a grid reject is "(cached)"

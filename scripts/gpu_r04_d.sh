@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round 4, session d: GPU tests + smoke on the new defaults (force-free: x power table, 5
+# waves/SIMD; Kerr: x power table), then a Kerr A/B over W / occupancy / table variants.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-r04_d}
+timeout -k 10 500 python -u -m pytest tests -v -m gpu --timeout 200 --timeout-method thread > gpurun_out/${T}_pytest_gpu.log 2>&1
+rc=$?; echo "PYTEST_RC=$rc"; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 4
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || exit 5
+timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu --no-extras > gpurun_out/${T}_ff.log 2>&1 || exit 6
+for v in "" knopt kpt1 kw4w6 kw4w5 kw3w6; do
+  PDEVAL_LIB=pde-engine_amd/lib/libpdeval${v:+_$v}.so timeout -k 10 200 python bench.py --steps 5 --warmup 2 --no-cpu --no-extras --problem kerr_magnetosphere > gpurun_out/${T}${v:+_$v}_kerr.log 2>&1 || exit 7
+done
+echo ALL_RC=0

@@ -122,6 +122,9 @@ def _filter_one(item):
     return out
 
 
+_EVIDENCE = False
+
+
 def _verdict_one(item):
     import sympy as sp
     idx, depth, s = item
@@ -130,6 +133,8 @@ def _verdict_one(item):
     t0 = time.time()
     signal.alarm(_TIMEOUT)
     try:
+        if _EVIDENCE:
+            d.validator._last_evidence = {}     # a fresh validator's state (kerr validator.py:380-381)
         u = sp.sympify(s, locals=d._sympify_locals)
         try:
             ok, reason = d.validator.validate(u, check_regularity=False, fast_point_only=False,
@@ -138,6 +143,8 @@ def _verdict_one(item):
         except TypeError:
             ok, reason = d.validator.validate(u, check_regularity=False, fast_point_only=False)
         rec.update(ok=bool(ok), reason=reason, timeout=False)
+        if _EVIDENCE:
+            rec['evidence'] = d.validator.last_evidence() if hasattr(d.validator, 'last_evidence') else None
     except _Timeout:
         rec.update(ok=None, reason=None, timeout=True)
     except Exception as e:  # noqa: BLE001  (the caller records status='error')
@@ -154,7 +161,7 @@ def read_stream(path):
 
 
 def main():
-    global _TIMEOUT
+    global _TIMEOUT, _EVIDENCE
     ap = argparse.ArgumentParser()
     ap.add_argument('mode', choices=['filters', 'verdicts'])
     ap.add_argument('--ref', default='/tmp/refcopy')
@@ -164,6 +171,7 @@ def main():
     ap.add_argument('--depth', type=int, default=None, help='only candidates of this depth')
     ap.add_argument('--sample', type=int, default=0, help='seeded sample size (0 = all)')
     ap.add_argument('--start', type=int, default=0, help='skip the first START input rows')
+    ap.add_argument('--evidence', action='store_true', help="also record the validator's last_evidence()")
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--timeout', type=int, default=60)
     ap.add_argument('--procs', type=int, default=os.cpu_count())
@@ -172,6 +180,7 @@ def main():
                     help='Kerr operator built with a = 0 (validator a argument = the number 0)')
     a = ap.parse_args()
     _TIMEOUT = a.timeout
+    _EVIDENCE = a.evidence
     make_scratch_copy('/root/reference', a.ref)
     t0 = time.time()
     if a.mode == 'filters':

@@ -1,0 +1,146 @@
+"""The host replay of the reference's symbolic stage (pde-engine_amd/pdeval/symbolic.py, the
+'text' / 'replay' modes of pdeval.batch.symbolic_stage), on the CPU.
+
+The reference's symbolic stage (problems/force_free/validator.py:404-427) is not a proof
+procedure: its branch on len(str(det_M)) chooses the reason text, and both branches have false
+negatives (a true solution it cannot reduce to 0).  The device decides det == 0 on the grid
+instead; the replay reproduces the reference where it matters.  Pinned here by:
+* the reference's own verdicts and texts on every decided fixture row that reached its
+  symbolic stage, against the replay's outputs recorded by scripts/replay_fixtures.py
+  (tests/golden/replay/ff_replay.jsonl, the product's code run ahead of time);
+* a live re-run of the replay on a seeded subset of those rows (the file stays pinned to the
+  code), including the two rows whose text / verdict only the replay reproduces
+  (golden_data.FF_DET_TEXT, golden_data.FF_D5_SYMBOLIC_DIVERGENCE);
+* the host step itself on a synthetic device result.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import golden_data as G
+from pdeval import problem_defs as P
+from pdeval import symbolic as S
+from pdeval.batch import symbolic_stage
+from pdeval.opcodes import CLS_ACCEPT, CLS_REJECT_GRID, CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC
+
+REPLAY = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'replay', 'ff_replay.jsonl')
+
+
+def _replay_rows():
+    with open(REPLAY) as f:
+        return {r['expr']: r for r in map(json.loads, f)}
+
+
+def _ref_symbolic_rows():
+    """Decided force-free reference rows whose reason comes from the symbolic stage."""
+    out = {}
+    for name in sorted(os.listdir(os.path.join(G.GOLDEN, "ref"))):
+        if not name.startswith('ff_') or not name.endswith('.jsonl'):
+            continue
+        for r in G.decided(G.ref_rows(name)):
+            rs = r['reason']
+            if r['ok'] or 'Lean could not' in rs or 'expanded det' in rs or 'simplify det' in rs:
+                out.setdefault(r['expr'], r)
+    return out
+
+
+def test_replay_outputs_equal_reference_on_every_symbolic_row():
+    rep, ref = _replay_rows(), _ref_symbolic_rows()
+    assert set(ref) <= set(rep), sorted(set(ref) - set(rep))[:5]
+    done = [e for e in ref if not rep[e]['timeout'] and rep[e]['ok'] is not None]
+    bad = [(e, ref[e]['reason'], rep[e]['reason']) for e in done
+           if (rep[e]['ok'], rep[e]['reason']) != (ref[e]['ok'], ref[e]['reason'])]
+    assert not bad, bad[:5]
+    # the replay finishes where the reference did (the same SymPy work), bar a few slow rows
+    assert len(done) >= 0.98 * len(ref), (len(done), len(ref))
+    # both known symbolic divergences of the device are reproduced by the replay
+    for e in G.FF_DET_TEXT | G.FF_D5_SYMBOLIC_DIVERGENCE:
+        assert e in done and rep[e]['reason'] == ref[e]['reason']
+
+
+def test_replay_live_subset_equals_recorded():
+    rep = _replay_rows()
+    fast = sorted(e for e, r in rep.items() if not r['timeout'] and r['t'] < 0.5)
+    sample = random.Random(0).sample(fast, min(12, len(fast))) + sorted(G.FF_DET_TEXT | G.FF_D5_SYMBOLIC_DIVERGENCE)
+    for e in sample:
+        got = S.replay_str(('force_free', e, True))
+        assert got is not None and (got[0], got[1]) == (rep[e]['ok'], rep[e]['reason']), (e, got, rep[e])
+
+
+def test_branch_texts():
+    pd = P.force_free()
+    # validator.py:404-427: the det string of rho/z - pow_3_2(rho**2/z**2) is 9,438 characters
+    # long -> the expand branch; sqrt(rho**2/z**2) -> the Lean branch, whose string round trip
+    # loses the assumptions (a false negative: det == 0)
+    d = S.ff_det(pd.parse('rho/z - pow_3_2(rho**2/z**2)'), pd.x, pd.y)
+    assert len(str(d)) >= S.DET_STR_LIMIT
+    assert S.ff_symbolic_stage(d, verdict=False) == (False, S.TEXT_EXPAND_FAIL)
+    d = S.ff_det(pd.parse('sqrt(rho**2/z**2)'), pd.x, pd.y)
+    assert len(str(d)) < S.DET_STR_LIMIT
+    assert S.ff_symbolic_stage(d) == (False, S.TEXT_LEAN_FAIL)
+    assert S.ff_replay(pd.parse('rho**2*z'), pd.x, pd.y) == (True, S.TEXT_LEAN_OK)
+    assert S.ff_det(pd.parse('3'), pd.x, pd.y) is None          # zero gradient: no det
+
+
+@pytest.mark.parametrize('mode', ['off', 'text', 'replay'])
+def test_symbolic_stage_host_step(mode):
+    pd = P.force_free()
+    items = ['exp_neg(rho/z - sqrt(rho/z))',      # device ACCEPT, reference: expanded det != 0
+             'rho/z - pow_3_2(rho**2/z**2)',      # device REJECT_GRID, reference: expanded text
+             'rho**2*z',                          # ACCEPT both
+             'rho*z',                             # point reject: never replayed
+             'sqrt(rho**2/z**2)']                 # device rule REJECT_SYMBOLIC, reference: Lean fails
+    st = np.array([CLS_ACCEPT, CLS_REJECT_GRID, CLS_ACCEPT, CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC], np.uint8)
+    out = {'status': st.copy(), 'verdict': st == CLS_ACCEPT}
+    rows = symbolic_stage(pd, items, out, mode, timeout=60)
+    ov = out.get('reason_override', {})
+    if mode == 'off':
+        assert rows == [] and not ov and np.array_equal(out['status'], st)
+        return
+    assert ov[1] == S.TEXT_EXPAND_FAIL and out['status'][1] == CLS_REJECT_GRID
+    assert 3 not in ov and out['status'][3] == CLS_REJECT_POINT
+    if mode == 'text':
+        assert set(ov) == {1} and np.array_equal(out['status'], st)
+    else:
+        assert out['status'][0] == CLS_REJECT_SYMBOLIC and not out['verdict'][0] and ov[0] == S.TEXT_EXPAND_FAIL
+        assert out['status'][2] == CLS_ACCEPT and out['verdict'][2] and ov[2] == S.TEXT_LEAN_OK
+        assert out['status'][4] == CLS_REJECT_SYMBOLIC and ov[4] == S.TEXT_LEAN_FAIL
+
+
+def _kerr_rows(name):
+    path = os.path.join(G.GOLDEN, 'ref', name)
+    if not os.path.exists(path):
+        pytest.skip(f'{name} not generated')
+    return G.decided(G.ref_rows(name))
+
+
+@pytest.mark.parametrize('name,spec', [('kerr_evidence.jsonl', ('M', 'a', '1', '1/10')),
+                                       ('kerr_op0_evidence.jsonl', ('M', '0', '1', '0'))])
+def test_kerr_text_and_evidence(name, spec):
+    """Kerr 'text' mode (pdeval.symbolic.kerr_text): the reference's reason texts with their
+    240-character residual repr (kerr validator.py:249-269, :308-315) and its last_evidence()
+    dict (:296-306), exactly, on rows the reference validated with evidence recorded
+    (gen_reference_verdicts.py --evidence): point rejects, grid rejects and accepts."""
+    # (a "(cached)" row is the reference instance's memo of an earlier, equal u: :274-281)
+    rows = [r for r in _kerr_rows(name) if '(cached)' not in r['reason']]
+    sample = random.Random(0).sample(rows, min(12, len(rows)))
+    sample += [r for r in rows if 'fast point' not in r['reason']][:8]
+    bad = []
+    for r in sample:
+        cls = 1 if 'fast point' in r['reason'] else (0 if r['ok'] else 2)
+        got = S.kerr_text((r['expr'], cls, spec))
+        assert got is not None, r['expr']
+        text, ev, zero = got
+        if cls:
+            if text != r['reason']:
+                bad.append((r['expr'], 'text', text, r['reason']))
+        else:
+            assert text is None and zero
+        if cls == 1:
+            assert ev is None and r['evidence'] == {}
+        elif ev != r['evidence']:
+            bad.append((r['expr'], 'evidence'))
+    assert not bad, bad[:3]
