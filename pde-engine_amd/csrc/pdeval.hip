@@ -687,7 +687,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         b.esc_count = cnt + esc;
         return b;
     };
-    const unsigned pgrid = (unsigned)std::min<int64_t>(4 * blocks, 8192);
+    // (small batches: enough blocks for every (candidate, part) of the split grid passes)
+    const unsigned pgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(4 * blocks, n * grid_parts(n)), 8192);
     // list-driven point kernels (one candidate per lane): enough blocks for the rare lists
     const unsigned lgrid = (unsigned)std::min<int64_t>((n + 63) / 64, 2048);
     a.defer_list = c->d_list[L_DEFER];
@@ -745,7 +746,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 2: stack 3, the lean interpreter over the L_DEFER list (64-thread blocks, 2 LDS
     // slots); what it does not take, the generic stack-3 kernel
     mark(3);
-    launch_grid_list(PROB, pgrid, s, follow(L_DEFER, L_DEFER2, L_ESC), c->d_list[L_SLOW2], cnt + L_SLOW2);
+    launch_grid_list(PROB, pgrid, s, follow(L_DEFER, L_DEFER2, L_ESC), c->d_list[L_SLOW2], cnt + L_SLOW2,
+                     grid_parts(n));
     HIPCHK(c, hipGetLastError());
     hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
                        dim3(64), (stack_lds<double, K, 3>(1)), s, follow(L_SLOW2, L_DEFER2, L_ESC));
@@ -763,7 +765,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         // the lean interpreter in complex arithmetic over the decoded programs; what it does not
         // take (point stage undecided, malformed) the generic complex kernel drains
         if (c->lean_cplx) {
-            launch_grid_cplx(pgrid, s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C), c->d_list[L_SLOW_C], cnt + L_SLOW_C);
+            launch_grid_cplx(pgrid, s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C), c->d_list[L_SLOW_C], cnt + L_SLOW_C,
+                             grid_parts(n));
             HIPCHK(c, hipGetLastError());
             hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
                                dim3(64), (stack_lds<cplx, K, 2>(1)), s, follow(L_SLOW_C, L_CPLX_DEEP, L_ESC_C));

@@ -395,10 +395,11 @@ template <class T, int K, int W, int MAXD> struct Lean {
             const bool more = !((w >> 20) & 1u);
             const int npc = pc + (int)((w >> 21) & 7u);
             // the next opcode word is fetched before this op's arithmetic (its scalar-load
-            // latency hides under it); the last op re-reads its own word
-            const int pn_at = more ? npc : pc;
-            const uint32_t wn = rd_word(dec + pn_at);
-            const double immn = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + pn_at + 1) : 0.0;
+            // latency hides under it); after the last op the three words past the program are
+            // read and ignored -- they exist: the decoded array is padded by 4 words
+            // (ensure_dec), so no select of the address is needed
+            const uint32_t wn = rd_word(dec + npc);
+            const double immn = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + npc + 1) : 0.0;
             const double cimm = PD_LEAN_IMM_PREFETCH ? imm : rd_imm(dec + pc + 1);
             const int pn = (int)((w >> 8) & 0xffu);   // POWN exponent / coordinate power n
             const bool on_y = (w >> 16) & 1u;         // coordinate-power axis
@@ -705,9 +706,17 @@ template <int PROB, int MAXD, class T = double> constexpr size_t grid_lds(int wa
 // The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots, jets
 // over T: double, or cplx for the force-free candidates not real at p* (the complex pass, whose
 // point stage point_list_kernel<.., cplx> decided).
+// Small batches (a handful of candidates: the inline driver's one validate() per candidate)
+// would leave all but a few SIMDs idle while one wave walks a candidate's 64 grid rows, so the
+// rows of each candidate are split over `parts` waves (contiguous ranges, whole W groups):
+// every part adds its counts into the candidate's accumulator (a.t2acc, zero between
+// launches, as tier 2's parts do) and the part that completes the candidate writes the
+// outputs and zeroes the accumulator.  Sums of counts and the max of maxima do not depend on
+// the split, so the outputs are those of one wave.
 template <int PROB, int MAXD, class T = double>
 __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int lane, T* stk,
-                                          int64_t* slow_list, int32_t* slow_count) {
+                                          int64_t* slow_list, int32_t* slow_count, int part = 0,
+                                          int parts = 1) {
     constexpr int K = grid_k<PROB>();
     constexpr int W = grid_w<PROB, MAXD>();
     constexpr bool CX = Real<T>::cplx_pass;
@@ -722,7 +731,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     if ((ps & 3) == P0_REJECT && !a.prm.full_grid) return;      // final after the point stage
     bool slow = !in_bounds || (hdr & 0xffu) != 0u || (ps & 3) == P0_NONE || (!CX && (hdr & PDEVAL_FLAG_COMPLEX));
     if (!slow && (int)((hdr >> 8) & 0xffu) > MAXD) {
-        if (lane == 0) list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
+        if (lane == 0 && part == 0) list_append(a.defer_list, a.defer_count, a.list_capacity, cand);
         return;
     }
     // the decoded program (decode_kernel, run before pass 1): 0xff = not for the lean passes;
@@ -734,7 +743,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
         u_sgn = (dh & 0x10000u) << 15;
     }
     if (slow) {
-        if (lane == 0) list_append(slow_list, slow_count, a.list_capacity, cand);
+        if (lane == 0 && part == 0) list_append(slow_list, slow_count, a.list_capacity, cand);
         return;
     }
     const int per_row = a.ny >> 6;
@@ -751,7 +760,10 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
         if (a.fp_pts[f] >= a.n_ref && r < 64) fp_rows |= 1ull << r;
     }
     if (a.nx > 64) fp_rows = ~0ull;
-    for (int row = 0; row < a.nx; row += W) {
+    // this part's rows: whole groups of W
+    const int groups = (a.nx + W - 1) / W;
+    const int row0 = W * (int)((int64_t)groups * part / parts), row1 = min(a.nx, W * (int)((int64_t)groups * (part + 1) / parts));
+    for (int row = row0; row < row1; row += W) {
         double x[W], inv_x[W];
 #pragma unroll
         for (int q = 0; q < W; ++q) {
@@ -816,7 +828,31 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
         }
     }
     qmax = wave_max(qmax);
-    const bool any_grad = __any(grad_nz) && !(ps & P0_CONST);
+    bool grad_any = __any(grad_nz);
+    if (parts > 1) {
+        int last = 0;
+        if (lane == 0) {
+            T2Acc* A = a.t2acc + cand;
+            atomicAdd(&A->nb1, nbad);
+            atomicAdd(&A->nfin, nfin);
+            atomicMax(&A->qmax_bits, (unsigned long long)__double_as_longlong(qmax));   // qmax >= 0
+            if (grad_any) atomicOr(&A->grad, 1u);
+            __threadfence();
+            if (atomicAdd(&A->done, 1) == parts - 1) {
+                __threadfence();
+                nbad = atomicAdd(&A->nb1, 0);
+                nfin = atomicAdd(&A->nfin, 0);
+                qmax = __longlong_as_double((long long)atomicMax(&A->qmax_bits, 0ull));
+                grad_any = atomicOr(&A->grad, 0u) != 0u;
+                A->nb1 = A->nfin = A->done = 0;   // ready for the next launch
+                A->grad = 0u;
+                A->qmax_bits = 0ull;
+                last = 1;
+            }
+        }
+        if (!__builtin_amdgcn_readfirstlane(last)) return;   // lane 0 is the first active lane
+    }
+    const bool any_grad = grad_any && !(ps & P0_CONST);
     if (lane == 0)
         grid_finish(a, cand, hdr, PROB, (ps & 3) == P0_REJECT, qmax, nbad, nfin, a.nx * a.ny - nfin, any_grad,
                     (ps & P0_CONST) != 0);
@@ -839,9 +875,12 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
 #ifndef PD_GRID_PERM
 #define PD_GRID_PERM 0
 #endif
-template <int PROB>
+// SPLIT: the small-batch instance (grid_body's parts); the full-batch instance has parts == 1
+// folded in, so its code is the one-wave-per-candidate kernel
+template <int PROB, bool SPLIT>
 __global__ __launch_bounds__(64 * PD_GRID_WPB, PROB == PDEVAL_PROBLEM_FORCE_FREE ? PD_GRID_WAVES_PER_SIMD : PD_KERR_WAVES_PER_SIMD)
-void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
+void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count, int parts_arg) {
+    const int parts = SPLIT ? parts_arg : 1;
 #ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
 #else
@@ -856,19 +895,25 @@ void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
     // measured 38.0 -> 38.7 ms with it, so Kerr keeps the launch order
     // (profiles/r02_bench_*_xcd*.log, r02_xcd_ff_pmc.json).
     int64_t blk = blockIdx.x;
-    if (PD_GRID_XCD && PROB == PDEVAL_PROBLEM_FORCE_FREE) {
+    if (PD_GRID_XCD && PROB == PDEVAL_PROBLEM_FORCE_FREE && parts == 1) {
         const int64_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
         blk = x * q + (x < r ? x : r) + blk / 8;
     }
-    const int64_t wi = blk * (blockDim.x >> 6) + wib;
+    int64_t wi = blk * (blockDim.x >> 6) + wib;
+    int part = 0;
+    if (parts > 1) {   // small batches: wave wi = (candidate, part)
+        part = (int)(wi % parts);
+        wi /= parts;
+    }
     if (wi >= a.n) return;
     const int64_t cand = (PD_GRID_PERM && a.perm) ? (int64_t)__builtin_amdgcn_readfirstlane(a.perm[wi]) : wi;
-    grid_body<PROB, 2>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
+    grid_body<PROB, 2>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, part, parts);
 }
 
 // pass 2: the stack-3 list a.list (count *a.list_count), persistent 64-thread blocks
-template <int PROB>
-__global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST_WAVES_PER_SIMD) void grid_list_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count) {
+template <int PROB, bool SPLIT>
+__global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST_WAVES_PER_SIMD) void grid_list_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count, int parts_arg) {
+    const int parts = SPLIT ? parts_arg : 1;
 #ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
 #else
@@ -877,9 +922,10 @@ __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST
     double* stk = reinterpret_cast<double*>(pd_lds);
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
-    for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+    for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
+        const int64_t wi = wp / parts;
         const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
-        grid_body<PROB, 3>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
+        grid_body<PROB, 3>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, (int)(wp % parts), parts);
     }
 }
 
@@ -889,8 +935,10 @@ __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST
 #ifndef PD_CPLX_WAVES_PER_SIMD
 #define PD_CPLX_WAVES_PER_SIMD 2
 #endif
+template <bool SPLIT>
 __global__ __launch_bounds__(64, PD_CPLX_WAVES_PER_SIMD) void grid_cplx_kernel(KernelArgs a, int64_t* slow_list,
-                                                                                int32_t* slow_count) {
+                                                                                int32_t* slow_count, int parts_arg) {
+    const int parts = SPLIT ? parts_arg : 1;
 #ifndef PD_HOST_SIM
     extern __shared__ __align__(16) unsigned char pd_lds[];
 #else
@@ -899,9 +947,11 @@ __global__ __launch_bounds__(64, PD_CPLX_WAVES_PER_SIMD) void grid_cplx_kernel(K
     cplx* stk = reinterpret_cast<cplx*>(pd_lds);
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
-    for (int64_t wi = blockIdx.x; wi < nwork; wi += gridDim.x) {
+    for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
+        const int64_t wi = wp / parts;
         const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
-        grid_body<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count);
+        grid_body<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count,
+                                                      (int)(wp % parts), parts);
     }
 }
 

@@ -7,15 +7,34 @@
 
 namespace pd {
 
+int grid_parts(int64_t n) {
+    // waves per candidate of the lean grid passes: 1 for batches that fill the chip; small
+    // batches split each candidate's 64 rows over up to 16 waves (~2k waves in flight)
+    int p = 1;
+    while (p < 16 && n * p * 2 <= 2048) p *= 2;
+    return p;
+}
+
 void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                  int64_t* slow_list, int32_t* slow_count) {
-    const unsigned blocks = (unsigned)((n + PD_GRID_WPB - 1) / PD_GRID_WPB);
-    if (problem == PDEVAL_PROBLEM_FORCE_FREE)
-        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(64 * PD_GRID_WPB),
-                           (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2>(PD_GRID_WPB)), s, a, slow_list, slow_count);
-    else
-        hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(64 * PD_GRID_WPB),
-                           (grid_lds<PDEVAL_PROBLEM_KERR, 2>(PD_GRID_WPB)), s, a, slow_list, slow_count);
+    const int parts = grid_parts(n);
+    const unsigned blocks = (unsigned)((n * parts + PD_GRID_WPB - 1) / PD_GRID_WPB);
+    const size_t lff = grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2>(PD_GRID_WPB), lk = grid_lds<PDEVAL_PROBLEM_KERR, 2>(PD_GRID_WPB);
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+        if (parts > 1)
+            hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE, true>), dim3(blocks), dim3(64 * PD_GRID_WPB), lff,
+                               s, a, slow_list, slow_count, parts);
+        else
+            hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE, false>), dim3(blocks), dim3(64 * PD_GRID_WPB), lff,
+                               s, a, slow_list, slow_count, 1);
+    } else {
+        if (parts > 1)
+            hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_KERR, true>), dim3(blocks), dim3(64 * PD_GRID_WPB), lk, s, a,
+                               slow_list, slow_count, parts);
+        else
+            hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_KERR, false>), dim3(blocks), dim3(64 * PD_GRID_WPB), lk, s, a,
+                               slow_list, slow_count, 1);
+    }
 }
 
 size_t ptab_bytes(int problem, int nx, int ny) {
@@ -38,19 +57,33 @@ void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a) {
         hipLaunchKernelGGL((decode_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(256), 0, s, a);
 }
 
-void launch_grid_cplx(unsigned blocks, hipStream_t s, const KernelArgs& a, int64_t* slow_list, int32_t* slow_count) {
-    hipLaunchKernelGGL(grid_cplx_kernel, dim3(blocks), dim3(64), (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(1)), s,
-                       a, slow_list, slow_count);
+void launch_grid_cplx(unsigned blocks, hipStream_t s, const KernelArgs& a, int64_t* slow_list, int32_t* slow_count,
+                      int parts) {
+    const size_t l = grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(1);
+    if (parts > 1)
+        hipLaunchKernelGGL(grid_cplx_kernel<true>, dim3(blocks), dim3(64), l, s, a, slow_list, slow_count, parts);
+    else
+        hipLaunchKernelGGL(grid_cplx_kernel<false>, dim3(blocks), dim3(64), l, s, a, slow_list, slow_count, 1);
 }
 
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
-                      int64_t* slow_list, int32_t* slow_count) {
-    if (problem == PDEVAL_PROBLEM_FORCE_FREE)
-        hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(blocks), dim3(64),
-                           (grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 3>(1)), s, a, slow_list, slow_count);
-    else
-        hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_KERR>), dim3(blocks), dim3(64),
-                           (grid_lds<PDEVAL_PROBLEM_KERR, 3>(1)), s, a, slow_list, slow_count);
+                      int64_t* slow_list, int32_t* slow_count, int parts) {
+    const size_t lff = grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 3>(1), lk = grid_lds<PDEVAL_PROBLEM_KERR, 3>(1);
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
+        if (parts > 1)
+            hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_FORCE_FREE, true>), dim3(blocks), dim3(64), lff, s, a,
+                               slow_list, slow_count, parts);
+        else
+            hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_FORCE_FREE, false>), dim3(blocks), dim3(64), lff, s, a,
+                               slow_list, slow_count, 1);
+    } else {
+        if (parts > 1)
+            hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_KERR, true>), dim3(blocks), dim3(64), lk, s, a,
+                               slow_list, slow_count, parts);
+        else
+            hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_KERR, false>), dim3(blocks), dim3(64), lk, s, a,
+                               slow_list, slow_count, 1);
+    }
 }
 
 }  // namespace pd

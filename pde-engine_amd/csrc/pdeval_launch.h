@@ -24,12 +24,16 @@ size_t ptab_bytes(int problem, int nx, int ny);
 void launch_ptab(int problem, const double* gx, const double* gy, int nx, int ny, double* tab, hipStream_t s);
 // decode every program for the lean passes (pdeval_grid.h decode_kernel) into a.dec
 void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a);
+// waves per candidate of the lean grid passes for a batch of n (small batches split each
+// candidate's rows over several waves, pdeval_grid.h grid_body)
+int grid_parts(int64_t n);
 void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
                  int64_t* slow_list, int32_t* slow_count);
 // the complex pass (force-free): persistent over the list a.list (L_CPLX), complex jets
-void launch_grid_cplx(unsigned blocks, hipStream_t s, const KernelArgs& a, int64_t* slow_list, int32_t* slow_count);
+void launch_grid_cplx(unsigned blocks, hipStream_t s, const KernelArgs& a, int64_t* slow_list, int32_t* slow_count,
+                      int parts);
 void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelArgs& a,
-                      int64_t* slow_list, int32_t* slow_count);
+                      int64_t* slow_list, int32_t* slow_count, int parts);
 // sort the batch by opcode sequence (pdeval_sort.hip): keys/idx hold 2 x n each, the
 // permutation ends in idx + n
 size_t sort_temp_bytes(int64_t cap);

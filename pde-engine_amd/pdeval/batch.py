@@ -31,7 +31,9 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import sympy as sp
 
+from . import hostpool
 from . import problem_defs as P
+from . import symbolic as S
 from .flatten import Unsupported
 from .opcodes import (CLS_ACCEPT, CLS_BAD_PROGRAM, CLS_NONFINITE_REF, CLS_REJECT_GRID,
                       CLS_REJECT_POINT, CLS_REJECT_SYMBOLIC, CLS_UNSUPPORTED, CLS_ZERO_GRADIENT, FLAG_NOCOORD,
@@ -152,8 +154,9 @@ def symbolic_zero_gradient(pd, items, out) -> List[int]:
                 np.isin(st, (CLS_ACCEPT, CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC)))
     idx = np.flatnonzero(flat)
     if len(idx) and all(isinstance(items[i], str) for i in idx):
-        from .hostpool import run   # strings: over the SymPy pool when it runs
-        zero = run(_zero_gradient_str, [(pd.slug, items[i]) for i in idx])
+        # strings: over the SymPy pool when it runs, even one at a time (the caller's thread then
+        # keeps the GIL free for the worker's other pipeline stages)
+        zero = hostpool.run(_zero_gradient_str, [(pd.slug, items[i]) for i in idx], min_items=1)
     else:
         zero = [_zero_gradient(pd, items[i]) for i in idx]
     rows = []
@@ -227,8 +230,7 @@ def kerr_symbolic_constant(pd, items, out, ops, off) -> List[int]:
     # pool when it runs, so the worker's pipeline does not stall); a check that hits it keeps
     # the device's class
     if all(isinstance(items[i], str) for i in sel):
-        from .hostpool import run
-        keeps = run(_kerr_keeps_coordinate_str, [(pd.slug, items[i]) for i in sel], min_items=1,
+        keeps = hostpool.run(_kerr_keeps_coordinate_str, [(pd.slug, items[i]) for i in sel], min_items=1,
                     item_timeout=KERR_SIMPLIFY_TIMEOUT_S, default=None)
     else:
         keeps = [_kerr_keeps_coordinate(pd, items[i]) for i in sel]
@@ -475,8 +477,9 @@ def symbolic_stage(pd, items, out, mode: str = 'text', timeout: float = SYMBOLIC
     """Force-free: the reference's symbolic stage replayed on the host (pdeval.symbolic) where
     it decides the verdict or the text (``problems/force_free/validator.py:404-427``):
 
-    * ``text``   -- grid rejects: SymPy's det_M and its printed length choose between "Invalid
-      (Lean could not simplify det to 0 symbolically)" and "Invalid (expanded det != 0)";
+    * ``text``   -- grid rejects and structural-rule rejects (REJECT_SYMBOLIC): SymPy's det_M and
+      its printed length choose between "Invalid (Lean could not simplify det to 0
+      symbolically)" and "Invalid (expanded det != 0)";
     * ``replay`` -- also every candidate the grid found zero (ACCEPT, REJECT_SYMBOLIC): the
       reference's symbolic verdict and text replace the device's (its false negatives, e.g. an
       expanded det that keeps sqrt(rho/z) and rho/z apart, become rejects).
@@ -498,20 +501,21 @@ def symbolic_stage(pd, items, out, mode: str = 'text', timeout: float = SYMBOLIC
     if pd.problem_id != PROBLEM_FORCE_FREE:
         return []
     st = np.asarray(out['status'])
-    cls = (CLS_REJECT_GRID,) if mode == 'text' else (CLS_REJECT_GRID, CLS_ACCEPT, CLS_REJECT_SYMBOLIC)
+    cls = (CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC) if mode == 'text' else (CLS_REJECT_GRID, CLS_ACCEPT, CLS_REJECT_SYMBOLIC)
     sel = np.flatnonzero(np.isin(st, cls)).tolist()
     if not sel:
         return []
-    from . import symbolic as S
-    args = [(pd.slug, items[i] if isinstance(items[i], str) else None, int(st[i]) != CLS_REJECT_GRID) for i in sel]
+    # the reference's symbolic verdict is needed for grid zeros in 'replay' mode only; a grid
+    # reject (det not zero) and, in 'text' mode, a structural-rule reject take the branch text
+    def need_verdict(c):
+        return mode == 'replay' and c != CLS_REJECT_GRID
+    args = [(pd.slug, items[i] if isinstance(items[i], str) else None, need_verdict(int(st[i]))) for i in sel]
     if all(a[1] is not None for a in args):
-        from .hostpool import run
-        res = run(S.replay_str, args, min_items=1, item_timeout=timeout, default=None)
+        res = hostpool.run(S.replay_str, args, min_items=1, item_timeout=timeout, default=None)
     else:
-        from .hostpool import _call_bounded
-        res = [_call_bounded(lambda it: S.ff_replay(it[0], pd.x, pd.y, it[1]),
+        res = [hostpool._call_bounded(lambda it: S.ff_replay(it[0], pd.x, pd.y, it[1]),
                              (items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i]),
-                              int(st[i]) != CLS_REJECT_GRID), timeout, None) for i in sel]
+                              need_verdict(int(st[i]))), timeout, None) for i in sel]
     ov = out.setdefault('reason_override', {})
     rows = []
     for i, r in zip(sel, res):
@@ -537,7 +541,6 @@ def kerr_operator_spec(pd, kerr) -> Tuple[str, str, str, str]:
 
 
 def _kerr_symbolic_stage(pd, items, out, mode, timeout, kerr) -> List[int]:
-    from . import symbolic as S
     if kerr is None:
         from ._lib import default_kerr_constants
         kerr = default_kerr_constants()
@@ -549,8 +552,7 @@ def _kerr_symbolic_stage(pd, items, out, mode, timeout, kerr) -> List[int]:
         return []
     strs = [items[i] if isinstance(items[i], str) else str(items[i]) for i in sel]
     args = [(s_, code[int(st[i])], spec) for s_, i in zip(strs, sel)]
-    from .hostpool import run
-    res = run(S.kerr_text, args, min_items=1, item_timeout=timeout, default=None)
+    res = hostpool.run(S.kerr_text, args, min_items=1, item_timeout=timeout, default=None)
     ov = out.setdefault('reason_override', {})
     evid = out.setdefault('evidence', {})
     rows = []

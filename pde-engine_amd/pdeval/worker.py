@@ -30,6 +30,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import sympy as sp
 
+from . import hostpool
+
 BASE_KWARGS = {'check_regularity': False, 'fast_point_only': False, 'lean_first': True,
                'defer_heavy_checks': True, 'enforce_anchor': False}
 
@@ -79,8 +81,10 @@ class KnownSolutionTagger:
         pairs = [(i, k) for i in np.flatnonzero(hits.any(axis=1)).tolist()
                  for k in np.flatnonzero(hits[i]).tolist()]
         if self.slug and pairs and all(isinstance(us[i], str) for i, _ in pairs):
-            from .hostpool import run   # strings: the SymPy confirmations over the pool
-            same = run(_confirm_str, [(self.slug, us[i], self.known_str[k]) for i, k in pairs])
+            # strings: the SymPy confirmations over the pool, even one at a time (the worker's
+            # result thread then keeps the GIL free for the compile and device threads)
+            same = hostpool.run(_confirm_str, [(self.slug, us[i], self.known_str[k]) for i, k in pairs],
+                                min_items=1)
         else:
             same = [_confirm(us[i], self.known[k][0], self.locals) for i, k in pairs]
         for (i, k), eq in zip(pairs, same):
@@ -120,7 +124,13 @@ def _confirm_str(args) -> bool:
         p = load_problem(slug)
         _LOCS[slug] = {**p.unary_ops, **p.symbols, **p.constants}
     locs = _LOCS[slug]
-    return _confirm(u, sp.sympify(known, locals=locs), locs)
+    kt = _KNOWN.get((slug, known))
+    if kt is None:
+        kt = _KNOWN[(slug, known)] = sp.sympify(known, locals=locs)
+    return _confirm(u, kt, locs)
+
+
+_KNOWN: Dict[Tuple[str, str], sp.Basic] = {}
 
 
 def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[str],
@@ -129,7 +139,6 @@ def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[s
                      local_workers: Optional[int] = None):
     """Worker process body (one per GPU).  Returns the number of candidates validated.
     ``local_workers``: GPU workers on this host (their SymPy pools share its cores)."""
-    from . import hostpool
     # the SymPy pool for declined strings and host checks, before the GPU is touched
     hostpool.start(local_workers=local_workers)
     try:

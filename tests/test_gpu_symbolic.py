@@ -1,0 +1,194 @@
+"""GPU tests of the named host modes that reproduce the reference's symbolic stage
+(pdeval.symbolic; plugin argument / env PDEVAL_SYMBOLIC) and of the small-batch graph path.
+
+* 'text'   -- force-free grid rejects get the reference's branch text ("Invalid (expanded det
+  != 0)" for a det string of 3,000+ characters, validator.py:404-427): golden_data.FF_DET_TEXT
+  is reproduced; Kerr rejects get the reference's exact text with its 240-character residual
+  repr and last_evidence() its evidence dict (kerr validator.py:249-306).  The reference
+  driver's Kerr run table replays through the inline loop (reason, method, math, evidence)
+  and the worker + writer (reason) with identical columns.
+* 'replay' -- the reference's symbolic verdict for grid zeros: the depth-5 false negative
+  golden_data.FF_D5_SYMBOLIC_DIVERGENCE is reproduced.
+* pdeval_validate_batch's HIP-graph path for batches of <= 64 candidates gives exactly the
+  direct path's outputs.
+"""
+import json
+import os
+import queue
+import random
+
+import numpy as np
+import pytest
+import sympy as sp
+
+import golden_data as G
+
+pytestmark = pytest.mark.gpu
+
+FF_SYMBOLIC_FILES = ('ff_d1.jsonl', 'ff_d2.jsonl', 'ff_d3_s500.jsonl', 'ff_d4_s500.jsonl', 'ff_d4_s2000.jsonl',
+                     'ff_d4_exp_quarter.jsonl', 'ff_edge.jsonl', 'ff_exp_power_forms.jsonl')
+
+
+def _locs(prob):
+    return {**prob.unary_ops, **prob.symbols, **prob.constants}
+
+
+def test_ff_text_mode_reject_texts():
+    """Every decided force-free fixture row the reference rejected in its symbolic stage, through
+    the plugin in 'text' mode: verdict and exact text (the FF_DET_TEXT row included)."""
+    from problems.force_free.validator import PreciseFoliationValidator
+    from problems import load_problem
+    prob = load_problem('force_free')
+    rows = [r for r in G.decided(G.ref_rows(*FF_SYMBOLIC_FILES))
+            if not r['ok'] and ('Lean could not' in r['reason'] or 'expanded det' in r['reason'])]
+    assert {r['expr'] for r in rows} >= G.FF_DET_TEXT
+    v = PreciseFoliationValidator(symbolic='text')
+    us = [sp.sympify(r['expr'], locals=_locs(prob)) for r in rows]
+    got = v.validate_batch(us, check_regularity=False, fast_point_only=False)
+    bad = [(r['expr'], r['reason'], g) for g, r in zip(got, rows) if (g[0], g[1]) != (r['ok'], r['reason'])]
+    assert not bad, bad[:5]
+    by = {r['expr']: g for g, r in zip(got, rows)}
+    for e in G.FF_DET_TEXT:
+        assert by[e] == (False, 'Invalid (expanded det != 0)')
+
+
+def test_ff_replay_mode_depth5():
+    """configs[3]'s depth in 'replay' mode: the reference's verdict and text on the depth-5
+    false negative and on a seeded sample of decided depth-5 rows that reached its symbolic
+    stage (the whole decided sample is checked on the CPU: test_oracle_golden.py)."""
+    from problems.force_free.validator import PreciseFoliationValidator
+    from problems import load_problem
+    prob = load_problem('force_free')
+    rows = G.decided(G.ref_rows(*G.FF_D5))
+    sym = [r for r in rows if r['ok'] or 'Lean could not' in r['reason'] or 'expanded det' in r['reason']]
+    pick = [r for r in sym if r['expr'] in G.FF_D5_SYMBOLIC_DIVERGENCE]
+    pick += random.Random(0).sample([r for r in sym if r['expr'] not in G.FF_D5_SYMBOLIC_DIVERGENCE], 16)
+    pick += random.Random(1).sample([r for r in rows if 'point check' in r['reason']], 8)
+    v = PreciseFoliationValidator(symbolic='replay')
+    us = [sp.sympify(r['expr'], locals=_locs(prob)) for r in pick]
+    got = v.validate_batch(us, check_regularity=False, fast_point_only=False)
+    bad = [(r['expr'], r['reason'], g) for g, r in zip(got, pick) if (g[0], g[1]) != (r['ok'], r['reason'])]
+    assert not bad, bad
+    # and 'off' keeps the device's (true) verdict on the false negative
+    off = PreciseFoliationValidator(symbolic='off')
+    e = sorted(G.FF_D5_SYMBOLIC_DIVERGENCE)[0]
+    assert off.validate(sp.sympify(e, locals=_locs(prob)), check_regularity=False)[0] is True
+
+
+def _kerr_driver_rows():
+    with open(os.path.join(G.GOLDEN, 'ref', 'driver_kerr_d2_rows.jsonl')) as f:
+        return [json.loads(l) for l in f]
+
+
+def test_kerr_driver_inline_rows_text_mode():
+    """The reference driver's Kerr run table (--problem kerr_magnetosphere --max-depth 2
+    --validators 0, tests/golden/gen_driver_rows.py) through its inline loop
+    (general_method_paper_reproduction.py:1288-1365) with this plugin in 'text' mode:
+    validation_status, is_valid, validation_reason, validator_method, validator_math and
+    validator_evidence (json of last_evidence()) identical on every row."""
+    from problems import load_problem
+    prob = load_problem('kerr_magnetosphere')
+    v = prob.validator
+    v.symbolic = 'text'
+    locs = _locs(prob)
+    coords = [prob.symbols.get(n, sp.Symbol(n)) for n in ('rho', 'z', 'r', 'x')]
+    rows = _kerr_driver_rows()
+    assert len(rows) == 306
+    bad = []
+    for r in rows:
+        u = sp.sympify(r['expression'], locals=locs)
+        if not any(u.has(c) for c in coords):                               # :1292-1294
+            ok, reason = False, 'constant-only (skipped)'
+        else:
+            ok, reason = v.validate(u, check_regularity=False, fast_point_only=False, lean_first=True,
+                                    defer_heavy_checks=True, enforce_anchor=False)
+        desc, ev = v.describe() or {}, v.last_evidence() or {}              # :1324-1335 (every row)
+        got = ('completed', int(bool(ok)), reason, desc.get('method_name'), desc.get('math_definition'),
+               json.dumps(ev))
+        want = (r['validation_status'], r['is_valid'], r['validation_reason'], r['validator_method'],
+                r['validator_math'], r['validator_evidence'])
+        if got != want:
+            bad.append((r['expression'], got[2][:80], want[2][:80]))
+    assert not bad, bad[:5]
+
+
+def test_kerr_driver_rows_worker_text_mode(tmp_path, monkeypatch):
+    """The same run table drained by the GPU worker pool and the centralized writer with
+    PDEVAL_SYMBOLIC=text: identical status, is_valid and reason (the worker's result tuples
+    carry no evidence: general_method_paper_reproduction.py:1799-1816)."""
+    import sqlite3
+    import threading
+    from pdeval import persist
+    from pdeval.worker import validator_worker
+    monkeypatch.setenv('PDEVAL_SYMBOLIC', 'text')
+    rows = [r for r in _kerr_driver_rows() if r['validation_reason'] != 'constant-only (skipped)']
+    db = os.path.join(tmp_path, 'run.db')
+    run_id = 'kerr-driver-replay'
+    table = persist.init_run_db(db, run_id, max_depth=2)
+    ids = persist.insert_candidates(db, table, [(r['expression'], r['normalized'], r['signature'], r['depth'])
+                                                for r in rows])
+    rq = queue.Queue()
+    wt = threading.Thread(target=persist.result_writer, args=(run_id, table, db, rq), kwargs={'poll_s': 0.05})
+    wt.start()
+    n = validator_worker(run_id, table, db, 'kerr_magnetosphere', None, rq, batch_size=64, idle_exit_s=1.0)
+    rq.put(None)
+    wt.join(timeout=120)
+    assert n == len(rows)
+    got = {r[0]: r[1:] for r in sqlite3.connect(db).execute(
+        f'SELECT id, validation_status, is_valid, validation_reason FROM {table}')}
+    bad = [(r['expression'], got[i][2][:60]) for i, r in zip(ids, rows)
+           if got[i] != (r['validation_status'], r['is_valid'], r['validation_reason'])]
+    assert not bad, bad[:5]
+
+
+def test_kerr_plugin_evidence_text_mode():
+    """last_evidence() after validate(u) in 'text' mode: the reference's dict for rows past
+    its fast point check (gen_reference_verdicts.py --evidence; a fresh validator per row)."""
+    from problems.kerr_magnetosphere.validator import KerrMagnetosphereValidator
+    from problems import load_problem
+    prob = load_problem('kerr_magnetosphere')
+    locs = _locs(prob)
+    s, c = prob.symbols, prob.constants
+    rows = [r for r in G.decided(G.ref_rows('kerr_evidence.jsonl'))
+            if 'fast point' not in r['reason'] and '(cached)' not in r['reason']][:12]
+    assert rows
+    for r in rows:
+        v = KerrMagnetosphereValidator(s['r'], s['x'], c['M'], c['a'], symbolic='text')
+        ok, reason = v.validate(sp.sympify(r['expr'], locals=locs), check_regularity=False,
+                                fast_point_only=False, lean_first=True, defer_heavy_checks=True,
+                                enforce_anchor=False)
+        assert (ok, reason) == (r['ok'], r['reason']), r['expr']
+        assert v.last_evidence() == r['evidence'], r['expr']
+
+
+def test_small_batch_graph_path_equals_direct():
+    """pdeval_validate_batch replays the launch chain of <= 64 candidates as a captured HIP
+    graph; a context created with PDEVAL_GRAPH=0 takes the direct path.  Every output is equal,
+    for batch sizes on both sides of the limit and after the buffers grow."""
+    from pdeval import problem_defs as P
+    from pdeval._lib import Context
+    pd_ = P.force_free()
+    strs = list(pd_.known_solutions) + [r['expr'] for r in G.decided(G.ref_rows('ff_edge.jsonl', 'ff_d2.jsonl'))]
+    strs += [r['expr'] for r in G.decided(G.ref_rows('ff_d4_s500.jsonl'))][:200]
+    ops, off, _ = P.compile_strings(pd_, strs)
+    g = Context(pd_.problem_id, device=0)
+    old = os.environ.get('PDEVAL_GRAPH')
+    os.environ['PDEVAL_GRAPH'] = '0'
+    try:
+        d = Context(pd_.problem_id, device=0)
+    finally:
+        if old is None:
+            del os.environ['PDEVAL_GRAPH']
+        else:
+            os.environ['PDEVAL_GRAPH'] = old
+    from pdeval.workload import gather_programs
+    try:
+        for start, n in ((0, 7), (0, 1), (0, 1), (3, 3), (7, 64), (71, 64), (0, 65), (0, 200), (9, 2), (5, 1), (0, 7)):
+            idx = (start + np.arange(n)) % len(strs)
+            o, f = gather_programs(ops, off, idx)
+            a, b = g.validate(o, f), d.validate(o, f)
+            for k in ('status', 'verdict', 'q_ref', 'res_ref', 'q_grid', 'n_bad', 'n_nonfinite', 'fingerprint'):
+                assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=a[k].dtype.kind == 'f'), (n, k)
+    finally:
+        g.close()
+        d.close()

@@ -103,7 +103,7 @@ def test_symbolic_stage_host_step(mode):
     assert ov[1] == S.TEXT_EXPAND_FAIL and out['status'][1] == CLS_REJECT_GRID
     assert 3 not in ov and out['status'][3] == CLS_REJECT_POINT
     if mode == 'text':
-        assert set(ov) == {1} and np.array_equal(out['status'], st)
+        assert set(ov) == {1, 4} and np.array_equal(out['status'], st) and ov[4] == S.TEXT_LEAN_FAIL
     else:
         assert out['status'][0] == CLS_REJECT_SYMBOLIC and not out['verdict'][0] and ov[0] == S.TEXT_EXPAND_FAIL
         assert out['status'][2] == CLS_ACCEPT and out['verdict'][2] and ov[2] == S.TEXT_LEAN_OK
@@ -118,7 +118,8 @@ def _kerr_rows(name):
 
 
 @pytest.mark.parametrize('name,spec', [('kerr_evidence.jsonl', ('M', 'a', '1', '1/10')),
-                                       ('kerr_op0_evidence.jsonl', ('M', '0', '1', '0'))])
+                                       # (the a = 0 operator fixtures were made with a_value = 1/10: gen_reference_verdicts.py)
+                                       ('kerr_op0_evidence.jsonl', ('M', '0', '1', '1/10'))])
 def test_kerr_text_and_evidence(name, spec):
     """Kerr 'text' mode (pdeval.symbolic.kerr_text): the reference's reason texts with their
     240-character residual repr (kerr validator.py:249-269, :308-315) and its last_evidence()
