@@ -319,6 +319,9 @@ template <int W> struct PowTab {
 #ifndef PD_LEAN_IMM_PREFETCH
 #define PD_LEAN_IMM_PREFETCH 1
 #endif
+#ifndef PD_PREFETCH_SELECT
+#define PD_PREFETCH_SELECT 0
+#endif
 template <class T, int K, int W, int MAXD> struct Lean {
     using O = JetOps<T, K>;
     using J = typename O::J;
@@ -398,8 +401,13 @@ template <class T, int K, int W, int MAXD> struct Lean {
             // latency hides under it); after the last op the three words past the program are
             // read and ignored -- they exist: the decoded array is padded by 4 words
             // (ensure_dec), so no select of the address is needed
-            const uint32_t wn = rd_word(dec + npc);
-            const double immn = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + npc + 1) : 0.0;
+#if PD_PREFETCH_SELECT   // (A/B: the round-3 form, re-reading its own word after the last op)
+            const int pn_at = more ? npc : pc;
+#else
+            const int pn_at = npc;
+#endif
+            const uint32_t wn = rd_word(dec + pn_at);
+            const double immn = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + pn_at + 1) : 0.0;
             const double cimm = PD_LEAN_IMM_PREFETCH ? imm : rd_imm(dec + pc + 1);
             const int pn = (int)((w >> 8) & 0xffu);   // POWN exponent / coordinate power n
             const bool on_y = (w >> 16) & 1u;         // coordinate-power axis
