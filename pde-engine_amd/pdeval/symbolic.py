@@ -141,6 +141,31 @@ def ff_replay(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol, verdict: bool = True) -
         return None
 
 
+def ff_point_stage(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol,
+                   point=(sp.Rational(4, 5), sp.Rational(6, 7))) -> Optional[Tuple[bool, str]]:
+    """The reference's point stage in SymPy (validator.py:349-402, fast_point_only off):
+    ``det_M.subs(p*)``, ``cancel(together(.))`` -- a Number decides it ("point check != 0") --
+    then ``simplify`` and ``abs(complex(evalf(50)))``: below 1e-20 it passes to the symbolic
+    stage (None here), else "Invalid (point check ≈ {:.2e})".
+
+    The device decides the point stage from the exact value of det_M at p* (double-double
+    tier), which is what ``det_M.subs(p*).evalf(50)`` gives.  SymPy's ``cancel``/``simplify``
+    of the substituted (radical-laden) number can return a different number -- a
+    point-check text the reference prints that is not the value of its own det at p*
+    (golden_data.FF_D5_POINT_TEXT_DIVERGENCE).  Not used by any mode: at seconds per candidate
+    it is for pinning such rows in tests."""
+    det_M = ff_det(u, rho, z)
+    if det_M is None:
+        return None
+    v = det_M.subs({rho: point[0], z: point[1]})
+    s = sp.cancel(sp.together(v))
+    if s.is_Number:
+        return None if s == 0 else (False, 'Invalid (point check != 0)')
+    s = sp.simplify(s)
+    d = abs(complex(s.evalf(50)))
+    return None if d < 1e-20 else (False, f'Invalid (point check ≈ {d:.2e})')
+
+
 _PDS: Dict[str, object] = {}
 
 

@@ -134,13 +134,21 @@ FF_COUNT_SLACK = {
 }
 
 # Depth 5 (configs[3]'s depth; the stream is not enumerable here): the reference's
-# verdicts on a seeded sample of 400 depth-5 strings of the stream's grammar
-# (gen_d5_sample.py -> streams/force_free_d5_sample.txt.gz -> ref/ff_d5_s400.jsonl; 399 rows:
-# the reference's validate on pow_3_2(pow_neg_3_2(z**2)/(-rho**2 + z**2 + 1)) ignored its 60 s
-# alarm and was still running when the generator's 2 h limit ended it).  One
-# decided row is a symbolic-stage false negative of the reference that no rule here restates:
-# u = exp(-rho/z + sqrt(rho/z)), a function of rho/z alone (det == 0), whose determinant string
-# is long enough for the reference to expand it (validator.py:407-426, "expanded det != 0")
-# and SymPy leaves sqrt(rho/z) terms un-merged.  The device accepts it (the true verdict).
-FF_D5 = ('ff_d5_s400.jsonl',)
+# verdicts on seeded depth-5 strings of the stream's grammar (gen_d5_sample.py ->
+# streams/force_free_d5_sample.txt.gz -> ref/ff_d5_s400.jsonl, the first 400 with a 60 s limit;
+# ref/ff_d5_s4000_t20.jsonl, the next 3,600 with a 20 s limit).  The rows the reference decided
+# in its symbolic stage against the true verdict -- its false negatives, e.g.
+# u = exp(-rho/z + sqrt(rho/z)), a function of rho/z alone (det == 0) whose determinant string is
+# long enough for the reference to expand it (validator.py:407-426, "expanded det != 0") while
+# SymPy leaves the sqrt(rho/z) terms un-merged -- are reproduced by the 'replay' mode
+# (pdeval/symbolic.py); the default mode gives the true verdict.
+FF_D5 = ('ff_d5_s400.jsonl', 'ff_d5_s4000_t20.jsonl')
 FF_D5_SYMBOLIC_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))'}
+# depth-5 point rejects whose reference text carries a number SymPy's cancel/simplify made up:
+# det_M.subs(p*).evalf(50) -- the exact value, what the device and the oracle print -- against
+# the reference's cancel(together(.)) -> simplify -> evalf pipeline (validator.py:366-394).
+# Same verdict; test_oracle_golden.test_point_text_divergence_is_sympys shows both numbers.
+FF_D5_POINT_TEXT_DIVERGENCE = {
+    '(pow_neg_3_2(sqrt(z) - z)) - (exp_neg(rho))': ('Invalid (point check ≈ 4.10e+03)',
+                                                    'Invalid (point check ≈ 6.13e+12)'),
+}
