@@ -34,7 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, 'tests'))
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (spec; MI355X_MICROARCH.md lists FP32 157.3 = 2x)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s"
-DOMINANT = 'grid_kernel<0>'   # pass 1 (force-free); Kerr: grid_kernel<1>
+DOMINANT = 'grid_kernel<0, false>'   # pass 1 (force-free, full-batch instance); Kerr: grid_kernel<1, false>
 
 
 def load_workload(problem):
@@ -121,7 +121,7 @@ def main():
     pid = PROBLEM_FORCE_FREE if a.problem == 'force_free' else PROBLEM_KERR
 
     slug = 'force_free' if pid == PROBLEM_FORCE_FREE else 'kerr_magnetosphere'
-    dominant = f'grid_kernel<{pid}>'
+    dominant = f'grid_kernel<{pid}, false>'
     wname, ops_all, off_all, exprs_all = load_workload(slug)
     nprog = len(off_all) - 1
     total = a.n * world
@@ -390,8 +390,9 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
     general_method_paper_reproduction.py:1756-1816, queue tuples in -> result tuples out):
     * process_batch, one queue-sized batch at a time (native compile, one device call,
       vectorized reasons, known-solution tags);
-    * process_batches, the worker loop's three-stage pipeline (batch k+2 compiles on host
-      threads while batch k+1 is on the device and batch k's tuples are built), at the
+    * process_batches, the worker loop's four-stage pipeline (later batches compile on host
+      threads while batch k+2 is on the device, batch k+1 gets its host steps and batch k
+      its tags and tuples), at the
       default queue batch and at larger ones -- its result tuples must equal process_batch's;
     * the inline path: one validate(sympify(s)) per candidate, as the driver's sequential loop
       calls it (:1299-1316), on a seeded sample."""

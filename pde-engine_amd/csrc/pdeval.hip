@@ -636,7 +636,11 @@ template <class T, int K, int MAXD> constexpr size_t tier2_lds() {
 
 template <int PROB>
 static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, const int64_t* d_off, int64_t n,
-                      const pdeval_params& prm, const pdeval_outputs& o, hipStream_t s) {
+                      const pdeval_params& prm, const pdeval_outputs& o, hipStream_t s,
+                      int dmax = PDEVAL_MAX_STACK) {
+    // dmax: the batch's largest program depth when the host knows it (pdeval_validate_batch
+    // checks every header); the kernels of the lists only deeper programs reach are skipped --
+    // they would read a zero count and exit (what a small batch mostly pays for is launches)
     auto mark = [&](int k) {
         if (c->timing) (void)hipEventRecord(c->ev[k], s);
     };
@@ -721,7 +725,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     HIPCHK(c, hipGetLastError());
     // the deep real programs, then (force-free) the complex list, operand stacks in private memory
     mark(1);
-    {
+    if (dmax > 2) {
         KernelArgs b = follow(L_PDEEP, -1, L_ESC);
         launch_point_list(PROB, 0, lgrid, s, b);
         HIPCHK(c, hipGetLastError());
@@ -746,18 +750,22 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 2: stack 3, the lean interpreter over the L_DEFER list (64-thread blocks, 2 LDS
     // slots); what it does not take, the generic stack-3 kernel
     mark(3);
-    launch_grid_list(PROB, pgrid, s, follow(L_DEFER, L_DEFER2, L_ESC), c->d_list[L_SLOW2], cnt + L_SLOW2,
-                     grid_parts(n));
-    HIPCHK(c, hipGetLastError());
-    hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
-                       dim3(64), (stack_lds<double, K, 3>(1)), s, follow(L_SLOW2, L_DEFER2, L_ESC));
-    HIPCHK(c, hipGetLastError());
+    if (dmax > 2) {
+        launch_grid_list(PROB, pgrid, s, follow(L_DEFER, L_DEFER2, L_ESC), c->d_list[L_SLOW2], cnt + L_SLOW2,
+                         grid_parts(n));
+        HIPCHK(c, hipGetLastError());
+        hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
+                           dim3(64), (stack_lds<double, K, 3>(1)), s, follow(L_SLOW2, L_DEFER2, L_ESC));
+        HIPCHK(c, hipGetLastError());
+    }
     // pass 3: stack 4..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
     mark(4);
-    hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
-                       dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
-                       (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
-    HIPCHK(c, hipGetLastError());
+    if (dmax > 3) {
+        hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
+                           dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
+                           (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
+        HIPCHK(c, hipGetLastError());
+    }
     if constexpr (FF) {
         // complex passes: candidates not real at the reference point, in complex arithmetic
         // (SymPy evaluates the point exactly, in the complex field: validator.py:363-402)
@@ -776,10 +784,12 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         }
         HIPCHK(c, hipGetLastError());
         mark(6);
-        hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),
-                           dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
-                           (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
-        HIPCHK(c, hipGetLastError());
+        if (dmax > 2) {
+            hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),
+                               dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
+                               (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
+            HIPCHK(c, hipGetLastError());
+        }
     } else {
         mark(5);
         mark(6);
@@ -792,13 +802,17 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
                        dim3(64), (tier2_lds<double, K, 2>()), s, t);
     HIPCHK(c, hipGetLastError());
     mark(8);
-    hipLaunchKernelGGL((tier2_kernel<PROB, double, 3, false, PD_T2_PARTS>), dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS, 4096)),
-                       dim3(64), (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
-    HIPCHK(c, hipGetLastError());
+    if (dmax > 2) {
+        hipLaunchKernelGGL((tier2_kernel<PROB, double, 3, false, PD_T2_PARTS>), dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS, 4096)),
+                           dim3(64), (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
+        HIPCHK(c, hipGetLastError());
+    }
     mark(9);
-    hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
-                       dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, follow(L_ESC_DEEP2, -1, L_ESC));
-    HIPCHK(c, hipGetLastError());
+    if (dmax > 3) {
+        hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
+                           dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, follow(L_ESC_DEEP2, -1, L_ESC));
+        HIPCHK(c, hipGetLastError());
+    }
     if constexpr (FF) {
         mark(10);
         hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4, false, PD_T2_PARTS_C>),
@@ -807,9 +821,11 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         HIPCHK(c, hipGetLastError());
         // complex programs of stack 5..8: operand stack in private memory (161 KiB of LDS would
         // not fit)
-        hipLaunchKernelGGL((tier2_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>), dim3((unsigned)std::min<int64_t>(n, 256)),
-                           dim3(64), 0, s, follow(L_ESC_C_DEEP, -1, L_ESC_C));
-        HIPCHK(c, hipGetLastError());
+        if (dmax > 4) {
+            hipLaunchKernelGGL((tier2_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>), dim3((unsigned)std::min<int64_t>(n, 256)),
+                               dim3(64), 0, s, follow(L_ESC_C_DEEP, -1, L_ESC_C));
+            HIPCHK(c, hipGetLastError());
+        }
     } else {
         mark(10);
     }
@@ -827,7 +843,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         hipLaunchKernelGGL(dd_collect_kernel<PROB>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
         HIPCHK(c, hipGetLastError());
         launch_dd_point(PROB, 0, lgrid, s, follow(L_DD, -1, L_ESC));
-        launch_dd_point(PROB, 1, lgrid, s, follow(L_DD8, -1, L_ESC));
+        if (dmax > 2) launch_dd_point(PROB, 1, lgrid, s, follow(L_DD8, -1, L_ESC));
         HIPCHK(c, hipGetLastError());
         if constexpr (FF) {
             launch_dd_point(PROB, 2, lgrid, s, follow(L_DDC, -1, L_ESC));
@@ -839,9 +855,9 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     return PDEVAL_OK;
 }
 
-extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words,
-                                      const int64_t* d_offsets, int64_t n, const pdeval_params* params,
-                                      const pdeval_outputs* d_out, void* stream, int zero_bits) {
+static int validate_device(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, const int64_t* d_offsets,
+                           int64_t n, const pdeval_params* params, const pdeval_outputs* d_out, void* stream,
+                           int zero_bits, int dmax) {
     if (!c || !d_out || n < 0 || (n > 0 && (!d_ops || !d_offsets)) || n_words < 0) {
         if (c) c->err = "pdeval_validate_device: bad argument";
         return PDEVAL_ERR_ARG;
@@ -865,8 +881,15 @@ extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64
     if (zero_bits && d_out->verdict_bits)
         HIPCHK(c, hipMemsetAsync(d_out->verdict_bits, 0, ((n + 31) / 32) * 4, s));
     if (c->problem == PDEVAL_PROBLEM_FORCE_FREE)
-        return launch_all<PDEVAL_PROBLEM_FORCE_FREE>(c, d_ops, n_words, d_offsets, n, prm, *d_out, s);
-    return launch_all<PDEVAL_PROBLEM_KERR>(c, d_ops, n_words, d_offsets, n, prm, *d_out, s);
+        return launch_all<PDEVAL_PROBLEM_FORCE_FREE>(c, d_ops, n_words, d_offsets, n, prm, *d_out, s, dmax);
+    return launch_all<PDEVAL_PROBLEM_KERR>(c, d_ops, n_words, d_offsets, n, prm, *d_out, s, dmax);
+}
+
+extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words,
+                                      const int64_t* d_offsets, int64_t n, const pdeval_params* params,
+                                      const pdeval_outputs* d_out, void* stream, int zero_bits) {
+    // device-resident programs: their depths are not known here, every pass is launched
+    return validate_device(c, d_ops, n_words, d_offsets, n, params, d_out, stream, zero_bits, PDEVAL_MAX_STACK);
 }
 
 // ---- small host batches (the plugin's one-candidate validate(), the inline driver loop
@@ -902,7 +925,7 @@ static int64_t outbuf_layout(const pdeval_ctx* c, int64_t n, pdeval_outputs* d) 
 }
 
 static int validate_small(pdeval_ctx* c, const int32_t* ops, int64_t n_words, const int64_t* offsets, int64_t n,
-                          const pdeval_params* params, pdeval_outputs* out) {
+                          const pdeval_params* params, pdeval_outputs* out, int dmax) {
     if (n_words > kSmallWords) return kGraphFallback;
     // fixed-capacity buffers (growing them drops every captured graph)
     if (c->hcap_words < kSmallWords || c->hcap_n < PD_GRAPH_MAX_N + 1) {
@@ -940,13 +963,15 @@ static int validate_small(pdeval_ctx* c, const int32_t* ops, int64_t n_words, co
     pdeval_params prm;
     if (params) prm = *params;
     else pdeval_default_params(c->problem, &prm);
-    // graph key: n and the parameter bytes (FNV-1a)
+    // graph key: n, the depth class and the parameter bytes (FNV-1a)
+    dmax = dmax <= 2 ? 2 : dmax <= 4 ? dmax : PDEVAL_MAX_STACK;
     uint64_t key = 1469598103934665603ull;
     auto mix = [&](const void* p, size_t len) {
         const uint8_t* b = (const uint8_t*)p;
         for (size_t i = 0; i < len; ++i) key = (key ^ b[i]) * 1099511628211ull;
     };
     mix(&n, sizeof(n));
+    mix(&dmax, sizeof(dmax));
     mix(&prm, sizeof(prm));
     pdeval_outputs d{};
     const int64_t need = outbuf_layout(c, n, &d);
@@ -968,8 +993,8 @@ static int validate_small(pdeval_ctx* c, const int32_t* ops, int64_t n_words, co
         if (hipMemsetAsync(d.verdict_bits, 0, ((n + 31) / 32) * 4, s) != hipSuccess) lrc = PDEVAL_ERR_HIP;
         if (lrc == PDEVAL_OK)
             lrc = c->problem == PDEVAL_PROBLEM_FORCE_FREE
-                      ? launch_all<PDEVAL_PROBLEM_FORCE_FREE>(c, c->d_ops, c->hcap_words, c->d_off, n, prm, d, s)
-                      : launch_all<PDEVAL_PROBLEM_KERR>(c, c->d_ops, c->hcap_words, c->d_off, n, prm, d, s);
+                      ? launch_all<PDEVAL_PROBLEM_FORCE_FREE>(c, c->d_ops, c->hcap_words, c->d_off, n, prm, d, s, dmax)
+                      : launch_all<PDEVAL_PROBLEM_KERR>(c, c->d_ops, c->hcap_words, c->d_off, n, prm, d, s, dmax);
         const hipError_t ee = hipStreamEndCapture(s, &g);
         hipGraphExec_t exec = nullptr;
         if (lrc != PDEVAL_OK || ee != hipSuccess || !g || hipGraphInstantiate(&exec, g, nullptr, nullptr, 0) != hipSuccess) {
@@ -1021,6 +1046,7 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
         c->err = "pdeval_validate_batch: offsets must start at 0 and end at n_words";
         return PDEVAL_ERR_ARG;
     }
+    int dmax = 0;
     for (int64_t i = 0; i < n; ++i) {
         if (offsets[i + 1] < offsets[i]) {
             c->err = "pdeval_validate_batch: offsets not monotone at " + std::to_string(i);
@@ -1032,10 +1058,11 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
                      std::to_string(d) + ")";
             return PDEVAL_ERR_PROGRAM;
         }
+        dmax = std::max(dmax, d);
     }
     HIPCHK(c, hipSetDevice(c->device));
     if (n <= PD_GRAPH_MAX_N && c->use_graph && !c->timing) {
-        const int rc = validate_small(c, ops, n_words, offsets, n, params, out);
+        const int rc = validate_small(c, ops, n_words, offsets, n, params, out, dmax);
         if (rc != kGraphFallback) return rc;
     }
     if (n_words > c->hcap_words) {
@@ -1079,7 +1106,7 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
     hipStream_t s = c->stream;
     HIPCHK(c, hipMemcpyAsync(c->d_ops, ops, n_words * sizeof(int32_t), hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_off, offsets, (n + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    int rc = pdeval_validate_device(c, c->d_ops, n_words, c->d_off, n, params, &d, s, 1);
+    int rc = validate_device(c, c->d_ops, n_words, c->d_off, n, params, &d, s, 1, dmax);
     if (rc) return rc;
     auto dl = [&](void* h, const void* dv, size_t bytes) -> int {
         if (h) HIPCHK(c, hipMemcpyAsync(h, dv, bytes, hipMemcpyDeviceToHost, s));

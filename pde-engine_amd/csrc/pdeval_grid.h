@@ -69,7 +69,8 @@ constexpr uint64_t kVarMask = op_bit(PDOP_MUL_X) | op_bit(PDOP_MUL_Y) | op_bit(P
 //                              the lean passes cannot take it (lean_prescan<3> fails)
 //   at each opcode position    op (bits 0-7), the word's own bits 8-16 (POWN / coordinate power
 //                              n, axis), the dispatch group (17-19), last-opcode bit (20), the
-//                              distance to the next opcode (21-23: 1, 3 or 5)
+//                              distance to the next opcode (21-23: 1, 3 or 5), and the dispatch
+//                              group again as one bit of 24-29 (PD_ONEHOT: one bit test each)
 //   after an immediate opcode  the immediate as a double (low word first), a problem constant
 //                              (PDEVAL_IMM_PRM) already resolved to the grid stage's value
 // The lean passes then read only the decoded array.
@@ -183,7 +184,8 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
             const uint32_t w2 = (uint32_t)prog[pc + len];
             const uint32_t op2 = w2 & 0xffu;
             if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || (PD_FUSE_PUSHC == 1 && op2 == PDOP_MUL_P)) {
-                dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << 21));
+                dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << 21) |
+                                    (1u << (24 + DG_PUSH)));
                 sg[d] = 1;
                 last = pc;
                 pc += len + 1;
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
             }
         }
         dec[pc] = (int32_t)(dop | (w & 0x1ff00u & ((kImmMask & b) ? 0u : ~0u)) | (dec_group(op_bit((int)dop)) << 17) |
-                            ((uint32_t)len << 21));
+                            ((uint32_t)len << 21) | (1u << (24 + dec_group(op_bit((int)dop)))));
         last = pc;
         pc += len;
     }
@@ -321,6 +323,19 @@ template <int W> struct PowTab {
 #endif
 #ifndef PD_PREFETCH_SELECT
 #define PD_PREFETCH_SELECT 0
+#endif
+#ifndef PD_ONEHOT
+#define PD_ONEHOT 1
+#endif
+// the force-free epilogue's 1/rho from the grid's reciprocal table (the value rcp() forms)
+// instead of a division per row
+#ifndef PD_EPI_TABLE_RCP
+#define PD_EPI_TABLE_RCP 1
+#endif
+// the per-point scaled residual by reciprocal + Newton steps instead of an IEEE division
+// (scaled_fast)
+#ifndef PD_FAST_SCALED
+#define PD_FAST_SCALED 0
 #endif
 template <class T, int K, int W, int MAXD> struct Lean {
     using O = JetOps<T, K>;
@@ -395,6 +410,12 @@ template <class T, int K, int W, int MAXD> struct Lean {
         for (;;) {
             const uint32_t op = w & 0xffu;
             const uint32_t grp = (w >> 17) & 7u;
+            // group tests: a bit test on the one-hot copy (s_bitcmp + branch) or a compare of
+            // the 3-bit field (extract + compare + branch)
+            auto in_grp = [&](uint32_t g) -> bool {
+                if constexpr (PD_ONEHOT) return (w >> (24 + g)) & 1u;
+                else return grp == g;
+            };
             const bool more = !((w >> 20) & 1u);
             const int npc = pc + (int)((w >> 21) & 7u);
             // the next opcode word is fetched before this op's arithmetic (its scalar-load
@@ -414,7 +435,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
             // dispatch: the decoded group, then the opcode, each a structured if/else (a flat
             // switch lowers to a compare tree whose unstructured joins the structurizer turns
             // into extra flow masks and copies)
-            if (grp == DG_PUSH) {
+            if (in_grp(DG_PUSH)) {
                 if (!first) {
                     if (RSLOT && d == 2) {
 #pragma unroll
@@ -483,7 +504,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::set_const(acc[q], cvt<T>(c));
                 }
-            } else if (grp == DG_CHEAP) {
+            } else if (in_grp(DG_CHEAP)) {
                 if (op == PDOP_ADDC) {
                     const double c = cimm;
 #pragma unroll
@@ -520,7 +541,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                         acc[q].c[ji(0, 1)] = acc[q].c[ji(0, 1)] + from_real<T>(-1.0);
                     }
                 }
-            } else if (grp == DG_POP) {
+            } else if (in_grp(DG_POP)) {
                 double pk[K + 1];
                 if (on_y) {
                     pco_y(pt, y, pn, pk);
@@ -533,7 +554,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                         O::template p_op<0>(op, acc[q], pk);
                     }
                 }
-            } else if (grp == DG_BIN) {
+            } else if (in_grp(DG_BIN)) {
                 const T* src = stk + (MAXD == 2 || RSLOT ? 0 : d - 2) * SLOT;
                 const bool from_reg = RSLOT && d == 3;
                 --d;
@@ -555,7 +576,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                     else if (op == PDOP_RDIV) O::rdiv(l, acc[q]);
                     else O::rsub(l, acc[q]);
                 }
-            } else if (grp == DG_VAR) {
+            } else if (in_grp(DG_VAR)) {
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
                     if (op == PDOP_DIV_Y) div_var(acc[q], y, inv_y, 1);
@@ -812,9 +833,10 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 if (W > 1 && row + q >= a.nx) break;                     // uniform
                 const int base = a.n_ref + (row + q) * a.ny + sl * 64;   // point index of lane 0
                 PointResult r;
-                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u[q].c, x[q]);
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE)
+                    r = PD_EPI_TABLE_RCP ? ff_epilogue_r<T>(u[q].c, inv_x[q]) : ff_epilogue<T>(u[q].c, x[q]);
                 else r = kerr_epilogue<T>(u[q].c, kv[q]);
-                const double qv = scaled(r.res_abs, r.scale);
+                const double qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
                 if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {

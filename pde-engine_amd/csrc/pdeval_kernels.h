@@ -574,9 +574,10 @@ template <class T, bool MAG> struct FFEpi {
         out[ji(0, 1)] = fmac(q00, fr01, q01 * fr00) + sgn(fmac(p00, fz01, p01 * fz00));
     }
 
-    // rho: R = double, or dd in the double-double point tier
-    template <class R> static PD_HD T eval(const T* u, R rho) {
-        const R r0 = rcp(rho);
+    // rho: R = double, or dd in the double-double point tier; r0 = rcp(rho) (the grid passes
+    // pass their row's correctly rounded 1/x from the host table, the same value)
+    template <class R> static PD_HD T eval(const T* u, R rho) { return eval_r(u, rcp(rho)); }
+    template <class R> static PD_HD T eval_r(const T* u, R r0) {
         // 1/rho jet in the rho direction: (-1)^i / rho^(i+1)
         const R ri[3] = {r0, r0 * r0 * (MAG ? 1.0 : -1.0), r0 * r0 * r0};
         T LA[3], LB[3];
@@ -628,7 +629,9 @@ template <class T, bool MAG> struct FFEpi {
     }
 };
 
-template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u, double rho) {
+// (inv_rho = rcp(rho): the lean grid passes read it from the grid's reciprocal table instead of
+// dividing once per row; ff_epilogue below divides)
+template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T* u, double inv_rho) {
     PointResult r;
 #ifdef PD_VAR_NO_EPI   // timing variant: no determinant at all (verdicts meaningless)
     {
@@ -641,7 +644,7 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u
         return r;
     }
 #endif
-    const T det = FFEpi<T, false>::eval(u, rho);
+    const T det = FFEpi<T, false>::eval_r(u, inv_rho);
     // keep the signed and the magnitude evaluations apart: interleaved, the scheduler keeps
     // both sets of intermediates live
     __builtin_amdgcn_sched_barrier(0);
@@ -653,9 +656,9 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u
         double m[15];
 #pragma unroll
         for (int i = 0; i < 15; ++i) m[i] = mag(u[i]);
-        S = FFEpi<double, true>::eval(m, rho);
+        S = FFEpi<double, true>::eval_r(m, inv_rho);
     } else {
-        S = FFEpi<double, true>::eval(u, rho);
+        S = FFEpi<double, true>::eval_r(u, inv_rho);
     }
 #endif
     r.res_abs = mag(det);
@@ -673,6 +676,10 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u
     for (int i = 0; i < 15; ++i) fin = fin && jet_coef_ok(u[i]);
     r.finite = fin;
     return r;
+}
+
+template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u, double rho) {
+    return ff_epilogue_r<T>(u, rcp(rho));
 }
 
 // Kerr surrogate: L[u] = k1 u_rr + k2 u_xx + k3 u_r + k4 u_x, coefficients per point.
@@ -713,6 +720,21 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue(const T*
 __device__ __forceinline__ double scaled(double res_abs, double S) {
     if (S > 0.0) return res_abs / S;
     return res_abs == 0.0 ? 0.0 : INFINITY;
+}
+
+// scaled() for the lean grid passes' per-point test: res_abs * 1/S with the hardware
+// reciprocal and two Newton steps (5 VALU against the 10 of the IEEE division sequence, which
+// the Kerr epilogue pays per point beside ~20 others).  Relative error ~2^-52 -- far below the
+// jets' own rounding, which the grid threshold and tier 2 already absorb; the exact division
+// for S outside [2^-1000, 2^1000] and for S == 0.
+__device__ __forceinline__ double scaled_fast(double res_abs, double S) {
+    if (S > 0x1p-1000 && S < 0x1p1000) {
+        double r = __builtin_amdgcn_rcp(S);
+        r = fma(r, fma(-S, r, 1.0), r);
+        r = fma(r, fma(-S, r, 1.0), r);
+        return res_abs * r;
+    }
+    return scaled(res_abs, S);
 }
 
 // ------------------------------------------------------------------ wave reductions

@@ -233,9 +233,11 @@ def compile_strings(pd_, strings: Sequence[str]):
     in-process.  Same (ops, offsets, notes)."""
     from . import problem_defs as P
     strings = list(strings)
-    if not active() or len(strings) < 8:
+    # (even one string: SymPy parses a declined string in ~1 ms holding the GIL, which the
+    # worker's other pipeline threads need; the pool round trip is cheaper than that stall)
+    if not active() or not strings:
         return P.compile_strings(pd_, strings)
-    k = max(1, min(_POOL.n * 2, len(strings) // 4))
+    k = max(1, min(_POOL.n * 2, (len(strings) + 1) // 2))
     step = (len(strings) + k - 1) // k
     args = [(pd_.slug, strings[i:i + step]) for i in range(0, len(strings), step)]
     parts = [p[0] if p is not None else _compile_chunk(a)

@@ -299,14 +299,18 @@ def _results(claimed, p, t, locs, tagger):
     return results
 
 
-def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 3, compilers: int = 2):
-    """process_batch over an iterable of claimed batches, pipelined in three stages on their
-    own threads: the next batches compile on the host (``compilers`` threads, so that one
-    batch's native compile -- C++ threads, GIL released -- overlaps another's wait for the
-    SymPy pool), the batch before them runs on the device (one library call, GIL released),
-    and the oldest one's host steps, verdict table, tags and result tuples are built on this
-    thread (host steps on the device thread measured slower: 855 k against 920-968 k/s).  ``depth`` batches are in flight at most.  Yields each batch's result tuples, in
-    order, identical to process_batch's.  An empty or None batch (the queue is idle) flushes."""
+def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 5, compilers: int = 3):
+    """process_batch over an iterable of claimed batches, pipelined in four stages on their own
+    threads: the next batches compile on the host (``compilers`` threads, so that one batch's
+    native compile -- C++ threads, GIL released -- overlaps another's wait for the SymPy pool),
+    the batch before them runs on the device (one library call, GIL released), the one before
+    that gets its host steps and verdict table (``finish``), and the oldest its known-solution
+    tags and result tuples.  The last two mostly wait for the SymPy pool processes
+    (pdeval.hostpool: gradient checks, simplify confirmations), so on separate threads those
+    waits overlap instead of adding up (r04_e profile: finish 0.071 s + results 0.097 s per
+    142 k rows on one thread was the pipeline's critical path).  ``depth`` batches are in
+    flight at most.  Yields each batch's result tuples, in order, identical to
+    process_batch's.  An empty or None batch (the queue is idle) flushes."""
     if not (hasattr(validator, 'validate_strings') and not kwargs.get('check_regularity', False)
             and not kwargs.get('fast_point_only', False)):
         for claimed in batches:
@@ -318,26 +322,33 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 3, co
     bv = validator._validator()
     sym = _symbolic_args(validator)
 
+    # each stage is one thread and takes its batches in submission order, so a stage only ever
+    # waits for an earlier stage's future of the same batch
     def run(pf):              # device thread: waits for its batch's compile, then runs it
         p = pf.result()
         return p, bv.run_prepared(p)
 
-    with ThreadPoolExecutor(max_workers=max(1, compilers)) as comp, ThreadPoolExecutor(max_workers=1) as dev:
-        inflight = deque()    # (claimed, future of (prepared, device result))
+    def fin(df):
+        p, r = df.result()
+        return p, bv.finish(p, r, **sym)
 
-        def pop():
-            c0, f0 = inflight.popleft()
-            p0, r0 = f0.result()
-            return _results(c0, p0, bv.finish(p0, r0, **sym), locs, tagger)
+    def res(claimed, ff):
+        p, t = ff.result()
+        return _results(claimed, p, t, locs, tagger)
+
+    with ThreadPoolExecutor(max_workers=max(1, compilers)) as comp, ThreadPoolExecutor(max_workers=1) as dev, \
+            ThreadPoolExecutor(max_workers=1) as fins, ThreadPoolExecutor(max_workers=1) as outs:
+        inflight = deque()    # futures of each batch's result tuples
 
         for claimed in batches:
             if not claimed:
                 while inflight:
-                    yield pop()
+                    yield inflight.popleft().result()
                 continue
             pf = comp.submit(bv.prepare_strings, [s for _, s in claimed])
-            inflight.append((claimed, dev.submit(run, pf)))
+            ff = fins.submit(fin, dev.submit(run, pf))
+            inflight.append(outs.submit(res, claimed, ff))
             while len(inflight) > depth:
-                yield pop()
+                yield inflight.popleft().result()
         while inflight:
-            yield pop()
+            yield inflight.popleft().result()

@@ -465,9 +465,11 @@ def test_kerr_constants_configs(cfg):
 def test_plugin_api_depth5_sample():
     """configs[3]'s depth: the reference's verdicts and reason texts on the seeded depth-5
     sample (golden_data.FF_D5) through the plugin on the GPU (default mode 'off'), except rows
-    the reference decided in its symbolic stage against the true verdict -- its false
-    negatives and branch texts -- each of which the 'replay' mode reproduces (the recorded
-    replay, tests/golden/replay/ff_replay.jsonl; the mode itself: tests/test_gpu_symbolic.py)."""
+    the reference decided in its symbolic stage where the grid and the structural rules differ
+    from SymPy (its false negatives, its branch texts, an Abs form the NONSMOOTH2D rule rejects
+    but SymPy proves) -- each of which the 'replay' mode reproduces (the recorded
+    replay, tests/golden/replay/ff_replay.jsonl; the mode itself: tests/test_gpu_symbolic.py),
+    and the point-check numbers of golden_data.FF_D5_POINT_TEXT_DIVERGENCE."""
     import json
     import os
     from problems import load_problem
@@ -480,7 +482,12 @@ def test_plugin_api_depth5_sample():
     with open(os.path.join(G.GOLDEN, 'replay', 'ff_replay.jsonl')) as f:
         rep = {r['expr']: r for r in map(json.loads, f)}
     bad = [r for g, r in zip(got, rows) if (g[0], g[1]) != (r['ok'], r['reason'])]
+    by = {r['expr']: g for g, r in zip(got, rows)}
     for r in bad:
+        if r['expr'] in G.FF_D5_POINT_TEXT_DIVERGENCE:
+            # the point-check number SymPy's simplify made up (test_oracle_golden.py)
+            assert (r['reason'], by[r['expr']][1]) == G.FF_D5_POINT_TEXT_DIVERGENCE[r['expr']]
+            continue
         x = rep.get(r['expr'])
         assert x is not None and (x['ok'], x['reason']) == (r['ok'], r['reason']), (r['expr'], r['reason'])
     assert {r['expr'] for r in bad} >= G.FF_D5_SYMBOLIC_DIVERGENCE

@@ -63,7 +63,8 @@ def test_ff_replay_mode_depth5():
     sym = [r for r in rows if r['ok'] or 'Lean could not' in r['reason'] or 'expanded det' in r['reason']]
     pick = [r for r in sym if r['expr'] in G.FF_D5_SYMBOLIC_DIVERGENCE]
     pick += random.Random(0).sample([r for r in sym if r['expr'] not in G.FF_D5_SYMBOLIC_DIVERGENCE], 16)
-    pick += random.Random(1).sample([r for r in rows if 'point check' in r['reason']], 8)
+    pick += random.Random(1).sample([r for r in rows if 'point check' in r['reason']
+                                     and r['expr'] not in G.FF_D5_POINT_TEXT_DIVERGENCE], 8)
     v = PreciseFoliationValidator(symbolic='replay')
     us = [sp.sympify(r['expr'], locals=_locs(prob)) for r in pick]
     got = v.validate_batch(us, check_regularity=False, fast_point_only=False)
@@ -161,10 +162,39 @@ def test_kerr_plugin_evidence_text_mode():
         assert v.last_evidence() == r['evidence'], r['expr']
 
 
+def _device_outputs(ctx, o, f, n_ref):
+    """pdeval_validate_device on device-resident programs: their depths are unknown to the host,
+    so every pass of the chain is launched."""
+    import torch
+    from pdeval import _lib
+    n = len(f) - 1
+    dev = torch.device('cuda:0')
+    d_ops = torch.from_numpy(np.ascontiguousarray(o, dtype=np.int32)).to(dev)
+    d_off = torch.from_numpy(np.ascontiguousarray(f, dtype=np.int64)).to(dev)
+    outs = dict(verdict_bits=torch.zeros(((n + 31) // 32) * 4, dtype=torch.uint8, device=dev),
+                status=torch.zeros(n, dtype=torch.uint8, device=dev),
+                q_ref=torch.zeros(n, dtype=torch.float64, device=dev),
+                res_ref=torch.zeros(n * n_ref, dtype=torch.float64, device=dev),
+                q_grid=torch.zeros(n, dtype=torch.float64, device=dev),
+                n_bad=torch.zeros(n, dtype=torch.int32, device=dev),
+                n_nonfinite=torch.zeros(n, dtype=torch.int32, device=dev),
+                fingerprint=torch.zeros(4 * n, dtype=torch.float64, device=dev))
+    d_out = _lib.Outputs(*[outs[k].data_ptr() for k, _ in _lib.Outputs._fields_])
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
+    ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out, stream=stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    r = {k: v.cpu().numpy() for k, v in outs.items()}
+    r['verdict'] = np.unpackbits(r.pop('verdict_bits'), bitorder='little')[:n].astype(bool)
+    return r
+
+
 def test_small_batch_graph_path_equals_direct():
     """pdeval_validate_batch replays the launch chain of <= 64 candidates as a captured HIP
     graph; a context created with PDEVAL_GRAPH=0 takes the direct path.  Every output is equal,
-    for batch sizes on both sides of the limit and after the buffers grow."""
+    for batch sizes on both sides of the limit and after the buffers grow.  Both skip the
+    passes only deeper programs reach (the host knows the batch's largest depth); the device
+    entry, which launches them all, gives the same outputs too."""
     from pdeval import problem_defs as P
     from pdeval._lib import Context
     pd_ = P.force_free()
@@ -187,8 +217,11 @@ def test_small_batch_graph_path_equals_direct():
             idx = (start + np.arange(n)) % len(strs)
             o, f = gather_programs(ops, off, idx)
             a, b = g.validate(o, f), d.validate(o, f)
+            full = _device_outputs(d, o, f, d.n_ref)
             for k in ('status', 'verdict', 'q_ref', 'res_ref', 'q_grid', 'n_bad', 'n_nonfinite', 'fingerprint'):
-                assert np.array_equal(np.asarray(a[k]), np.asarray(b[k]), equal_nan=a[k].dtype.kind == 'f'), (n, k)
+                x = np.asarray(a[k])
+                assert np.array_equal(x, np.asarray(b[k]), equal_nan=x.dtype.kind == 'f'), (n, k)
+                assert np.array_equal(x.ravel(), full[k].ravel(), equal_nan=x.dtype.kind == 'f'), (n, k, 'device')
     finally:
         g.close()
         d.close()
