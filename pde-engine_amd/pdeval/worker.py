@@ -299,7 +299,7 @@ def _results(claimed, p, t, locs, tagger):
     return results
 
 
-def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 5, compilers: int = 3):
+def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, compilers: int = 4):
     """process_batch over an iterable of claimed batches, pipelined in four stages on their own
     threads: the next batches compile on the host (``compilers`` threads, so that one batch's
     native compile -- C++ threads, GIL released -- overlaps another's wait for the SymPy pool),

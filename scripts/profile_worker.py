@@ -39,7 +39,7 @@ def main():
         st['prepare'] += t1 - t0; st['device'] += t2 - t1; st['finish'] += t3 - t2; st['results'] += t4 - t3
     print('stage seconds (batch %d):' % b, {k: round(v, 4) for k, v in st.items()})
     # pipeline shapes (depth, compile threads), no profiler; the first is process_batches' default
-    for depth, comp in ((5, 3), (4, 2), (6, 4), (8, 4)):
+    for depth, comp in ((8, 4), (12, 6), (16, 8)):
         t0 = time.perf_counter()
         n = sum(len(r) for r in process_batches((items[k:k + b] for k in range(0, len(items), b)),
                                                 prob.validator, kw, locs, tagger, depth=depth, compilers=comp))
