@@ -46,7 +46,10 @@ enum {
     L_SLOW = 13,      // lean grid pass -> the generic stack-2 kernel (malformed / undecided)
     L_SLOW2 = 14,     // lean stack-3 pass -> the generic stack-3 kernel
     L_SLOW_C = 15,    // lean complex pass -> the generic complex stack-2 kernel
-    PD_N_LISTS = 16
+    L_DDL = 16,       // the late double-double lists (provisional point passes, after the
+    L_DDLC = 17,      // grid): real, complex, real stack 3..8; L_DD / L_DDC / L_DD8 are the
+    L_DDL8 = 18,      // early ones (P0_DD, beside the grid passes on the side stream)
+    PD_N_LISTS = 19
 };
 
 namespace {
@@ -61,6 +64,12 @@ struct pdeval_ctx {
     int n_ref = 0, n_pts = 0;
     int fp_pts[PDEVAL_FP_N] = {0, 0, 0, 0};
     hipStream_t stream = nullptr;
+    // the early double-double tier runs on `side`, forked after the point stage and joined
+    // before the classes are final (env PDEVAL_DD_EARLY=0: one tier after the grid, A/B)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool dd_early = true;
+    uint8_t* d_ddps = nullptr;      // the early tier's classes, capacity cap
     double ref_x[4] = {0, 0, 0, 0}, ref_y[4] = {0, 0, 0, 0};
     dd ref_xd[4] = {}, ref_yd[4] = {};   // the reference points as double-doubles
     dd kc_ref[16] = {};                  // Kerr operator coefficients there, double-double
@@ -384,8 +393,14 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_SORT")) c->sort = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_LEAN_CPLX")) c->lean_cplx = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_GRAPH")) c->use_graph = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_DD_EARLY")) c->dd_early = atoi(v) != 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
+    if ((e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess)
+        return fail("hipStreamCreate", e);
+    if ((e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming)) != hipSuccess)
+        return fail("hipEventCreate", e);
     if ((e = hipMalloc(&c->d_gx, 2 * nx * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc(&c->d_gy, ny * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
     if (problem_id == PDEVAL_PROBLEM_KERR &&
@@ -406,10 +421,12 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (!c) return PDEVAL_ERR_ARG;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->comm) pdeval_comm_destroy(c);
     for (int64_t* l : c->d_list)
         if (l) (void)hipFree(l);
     if (c->d_pstate) (void)hipFree(c->d_pstate);
+    if (c->d_ddps) (void)hipFree(c->d_ddps);
     if (c->d_dec) (void)hipFree(c->d_dec);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
@@ -425,6 +442,9 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t& e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PDEVAL_OK;
@@ -592,6 +612,9 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (c->d_pstate) (void)hipFree(c->d_pstate);
     c->d_pstate = nullptr;
     HIPCHK(c, hipMalloc(&c->d_pstate, cap));
+    if (c->d_ddps) (void)hipFree(c->d_ddps);
+    c->d_ddps = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_ddps, cap));
     if (c->d_status) (void)hipFree(c->d_status);
     c->d_status = nullptr;
     HIPCHK(c, hipMalloc(&c->d_status, cap));
@@ -633,6 +656,10 @@ template <class T, int K, int MAXD> constexpr size_t stack_lds(int waves) {
 template <class T, int K, int MAXD> constexpr size_t tier2_lds() {
     return (size_t)(MAXD - 1) * ((K + 1) * (K + 2) / 2) * 64 * (sizeof(T) + sizeof(double));
 }
+
+#ifndef PD_DD_EARLY_MIN_N
+#define PD_DD_EARLY_MIN_N 1024
+#endif
 
 template <int PROB>
 static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, const int64_t* d_off, int64_t n,
@@ -702,6 +729,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.esc_list = c->d_list[L_ESC];
     a.esc_count = cnt + L_ESC;
     a.pstate = c->d_pstate;
+    a.ddps = c->d_ddps;
     a.pdeep_list = c->d_list[L_PDEEP];
     a.pdeep_count = cnt + L_PDEEP;
     a.noise_ref = c->d_noise;
@@ -734,6 +762,35 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         KernelArgs b = follow(L_CPLX, -1, L_ESC_C);
         launch_point_list(PROB, 1, lgrid, s, b);
         HIPCHK(c, hipGetLastError());
+    }
+    // the double-double lists: early = L_DD / L_DDC / L_DD8, late = L_DDL / L_DDLC / L_DDL8
+    auto dd_lists = [&](int l0, int lc, int l8) {
+        KernelArgs b = a;
+        b.defer_list = c->d_list[l0];
+        b.defer_count = cnt + l0;
+        b.cplx_list = c->d_list[lc];   // (Kerr: never appended to, count 0)
+        b.cplx_count = cnt + lc;
+        b.esc_list = c->d_list[l8];
+        b.esc_count = cnt + l8;
+        return b;
+    };
+    const unsigned cgrid = (unsigned)((n + 255) / 256);
+    // (below ~1,000 candidates the double-double tier is short and the fork only adds launches:
+    // 512 candidates 2.40 vs 2.36 ms, 1,024: 2.89 vs 3.24 ms, profiles/r04_k_device_batch.log)
+    const bool early = c->dd_early && n >= PD_DD_EARLY_MIN_N;
+    if (early) {
+        // ---- the early double-double tier (pdeval_point.h): the candidates the point stage
+        // left undecided or not accurate enough in fp64 are known now, so their evaluation runs
+        // on the side stream beside the grid passes (classes to ddps, applied after the grid)
+        hipLaunchKernelGGL((dd_collect_kernel<PROB, DD_EARLY>), dim3(cgrid), dim3(256), 0, s, dd_lists(L_DD, L_DDC, L_DD8));
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev_fork, s));
+        HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+        launch_dd_point(PROB, 0, lgrid, c->side, follow(L_DD, -1, L_ESC), true);
+        if (dmax > 2) launch_dd_point(PROB, 1, lgrid, c->side, follow(L_DD8, -1, L_ESC), true);
+        if constexpr (FF) launch_dd_point(PROB, 2, lgrid, c->side, follow(L_DDC, -1, L_ESC), true);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev_join, c->side));
     }
     // ---- the grid stage
     // pass 1: programs whose stack fits 2 jets (99 % of force-free depth 4), one wave per
@@ -832,23 +889,25 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // ---- the point stage's double-double tier (pdeval_point.h): candidates fp64 left
     // undecided, and provisional point passes whose grid stage rejected
     mark(11);
-    {
-        KernelArgs b = a;
-        b.defer_list = c->d_list[L_DD];
-        b.defer_count = cnt + L_DD;
-        b.cplx_list = c->d_list[L_DDC];
-        b.cplx_count = cnt + L_DDC;
-        b.esc_list = c->d_list[L_DD8];
-        b.esc_count = cnt + L_DD8;
-        hipLaunchKernelGGL(dd_collect_kernel<PROB>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, b);
+    if (early) {
+        // join the side stream; the late lists (provisional point passes the grid classes
+        // now make relevant), then the early tier's classes applied to the final grid classes
+        HIPCHK(c, hipStreamWaitEvent(s, c->ev_join, 0));
+        hipLaunchKernelGGL((dd_collect_kernel<PROB, DD_LATE>), dim3(cgrid), dim3(256), 0, s, dd_lists(L_DDL, L_DDLC, L_DDL8));
+        HIPCHK(c, hipGetLastError());
+        launch_dd_point(PROB, 0, lgrid, s, follow(L_DDL, -1, L_ESC));
+        if (dmax > 2) launch_dd_point(PROB, 1, lgrid, s, follow(L_DDL8, -1, L_ESC));
+        if constexpr (FF) launch_dd_point(PROB, 2, lgrid, s, follow(L_DDLC, -1, L_ESC));
+        HIPCHK(c, hipGetLastError());
+        launch_dd_apply(PROB, (unsigned)std::min<int64_t>(cgrid, 1024), s, dd_lists(L_DD, L_DDC, L_DD8));
+        HIPCHK(c, hipGetLastError());
+    } else {
+        hipLaunchKernelGGL((dd_collect_kernel<PROB, DD_ALL>), dim3(cgrid), dim3(256), 0, s, dd_lists(L_DD, L_DDC, L_DD8));
         HIPCHK(c, hipGetLastError());
         launch_dd_point(PROB, 0, lgrid, s, follow(L_DD, -1, L_ESC));
         if (dmax > 2) launch_dd_point(PROB, 1, lgrid, s, follow(L_DD8, -1, L_ESC));
+        if constexpr (FF) launch_dd_point(PROB, 2, lgrid, s, follow(L_DDC, -1, L_ESC));
         HIPCHK(c, hipGetLastError());
-        if constexpr (FF) {
-            launch_dd_point(PROB, 2, lgrid, s, follow(L_DDC, -1, L_ESC));
-            HIPCHK(c, hipGetLastError());
-        }
     }
     mark(PDEVAL_N_PASSES);
     c->ev_recorded = c->timing ? 1 : 0;

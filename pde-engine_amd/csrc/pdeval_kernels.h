@@ -71,6 +71,7 @@ struct KernelArgs {
     int64_t* esc_list;          // tier-2 escalations: cand | ESC_* flags << 48
     int32_t* esc_count;
     uint8_t* pstate;            // point-stage state per candidate (P0_*), or NULL
+    uint8_t* ddps;              // the early double-double tier's result per candidate (dd_point_kernel<DEFER>)
     int64_t* pdeep_list;        // real programs deeper than pass 0's stack: the deep point pass
     int32_t* pdeep_count;
     double* noise_ref;          // n * n_ref fp64 noise bounds at the reference points (point stage)

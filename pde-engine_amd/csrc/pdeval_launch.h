@@ -12,7 +12,9 @@ namespace pd {
 void launch_point_list(int problem, int cplx, unsigned grid, hipStream_t s, const KernelArgs& a);
 // double-double tier over a device list: kind 0 real programs of stack <= 2 (LDS stack),
 // 1 deeper real programs, 2 complex (force-free only)
-void launch_dd_point(int problem, int kind, unsigned grid, hipStream_t s, const KernelArgs& a);
+// defer: the early tier's kernels (classes to a.ddps, dd_apply_kernel applies them)
+void launch_dd_point(int problem, int kind, unsigned grid, hipStream_t s, const KernelArgs& a, bool defer = false);
+void launch_dd_apply(int problem, unsigned grid, hipStream_t s, const KernelArgs& a);
 // diagnostic: one program at the reference points in precision tier 0..3 (pdeval_point_eval)
 void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a, const int32_t* prog,
                        int plen, double* out, uint8_t* state);

@@ -398,20 +398,33 @@ __device__ __forceinline__ void nz_reject(const KernelArgs& a, int64_t cand) {
     if (a.out.verdict_bits) atomicAnd((uint32_t*)a.out.verdict_bits + (cand >> 5), ~(1u << (cand & 31)));
 }
 
-template <int PROB>
+// The tier-B lists.  EARLY (right after the point stage, before the grid): the candidates the
+// point stage left undecided or not accurate enough in fp64 (P0_DD) -- known before any grid
+// pass, so their double-double evaluation runs on a second stream beside the grid passes
+// (dd_point_kernel<DEFER>) and dd_apply_kernel applies it once the classes are final.  LATE
+// (after the grid): the provisional point passes (P0_PROV) whose grid class the double-double
+// value may still override; and the P0_NZ accepts.
+// MODE: DD_ALL (one tier after the grid: both kinds), DD_EARLY, DD_LATE.
+enum { DD_ALL = 0, DD_EARLY = 1, DD_LATE = 2 };
+template <int PROB, int MODE>
 __global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a) {
     const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= a.n) return;
     const int64_t cand = a.perm ? (int64_t)a.perm[li] : li;   // lists in shape order
     const uint8_t ps = a.pstate[cand];
     if ((ps & 3) == P0_NONE) return;
-    const uint8_t st = a.out.status[cand];
-    const bool need = (ps & P0_DD) ||
-                      ((ps & P0_PROV) && (st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||
-                                            st == PDEVAL_CLS_REJECT_SYMBOLIC));
-    if (!need) {
-        if ((ps & 3) == P0_PASS && (ps & P0_NZ) && st == PDEVAL_CLS_ACCEPT) nz_reject(a, cand);
-        return;
+    if (MODE == DD_EARLY) {
+        if (!(ps & P0_DD)) return;
+    } else {
+        if (MODE == DD_LATE && (ps & P0_DD)) return;           // the early tier took it
+        const uint8_t st = a.out.status[cand];
+        const bool need = (MODE == DD_ALL && (ps & P0_DD)) ||
+                          ((ps & P0_PROV) && (st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||
+                                                st == PDEVAL_CLS_REJECT_SYMBOLIC));
+        if (!need) {
+            if ((ps & 3) == P0_PASS && (ps & P0_NZ) && st == PDEVAL_CLS_ACCEPT) nz_reject(a, cand);
+            return;
+        }
     }
     if (ps & P0_CPLX) {
         list_append(a.cplx_list, a.cplx_count, a.list_capacity, cand);
@@ -617,7 +630,29 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
 #ifndef PD_DD2_WAVES
 #define PD_DD2_WAVES 2
 #endif
-template <int PROB, class T, int MAXD>
+// the double-double class s of a candidate, applied to its final grid class
+__device__ __forceinline__ void dd_apply_one(const KernelArgs& a, int64_t cand, uint8_t s) {
+    const uint8_t st = a.out.status ? a.out.status[cand] : (uint8_t)PDEVAL_CLS_ACCEPT;
+    // the reference checks the gradient (and Kerr the constant) before the point stage
+    const bool overridable = st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||
+                             st == PDEVAL_CLS_REJECT_SYMBOLIC;
+    if ((s & 3) == P0_REJECT && overridable) {
+        write_point_reject(a, cand);
+        if (a.out.verdict_bits)
+            atomicAnd((uint32_t*)a.out.verdict_bits + (cand >> 5), ~(1u << (cand & 31)));
+    } else if ((s & 3) == P0_PASS && (s & P0_NZ) && st == PDEVAL_CLS_ACCEPT) {
+        nz_reject(a, cand);
+    }
+    a.pstate[cand] = (uint8_t)((a.pstate[cand] & ~(3 | P0_DD | P0_PROV | P0_NZ)) | s);
+}
+
+// "keep the fp64 decision" in a.ddps (never a final class: those have no P0_DD bit)
+constexpr uint8_t kDdKeep = 0xfe;
+
+// DEFER (the early lists, on the second stream while the grid passes run): the class goes to
+// a.ddps[cand] and dd_apply_kernel applies it after the grid; nothing else the grid passes
+// read or write is touched here (res_ref, q_ref and the p* fingerprint are the point stage's).
+template <int PROB, class T, int MAXD, bool DEFER = false>
 __global__ __launch_bounds__(64, MAXD == 2 ? PD_DD2_WAVES : 1) void dd_point_kernel(KernelArgs a) {
     constexpr int K = (PROB == PDEVAL_PROBLEM_FORCE_FREE) ? 4 : 2;
     constexpr int NC = nc(K);
@@ -635,24 +670,35 @@ __global__ __launch_bounds__(64, MAXD == 2 ? PD_DD2_WAVES : 1) void dd_point_ker
          wi += (int64_t)gridDim.x * blockDim.x) {
         const int64_t cand = a.list[wi];
         int64_t beg, end;
-        if (!prog_bounds(a, cand, &beg, &end)) continue;
-        const int32_t* prog = a.ops + beg;
-        const uint32_t hdr = (uint32_t)prog[0];
-        if ((int)((hdr >> 8) & 0xffu) > MAXD) continue;     // (the collect pass routes by depth)
-        const uint8_t s = dd_point_stage<PROB, T, MAXD>(a, cand, prog, (int)(end - beg), hdr, stk);
-        if (s == P0_NONE) continue;   // not finite: keep the fp64 decision
-        const uint8_t st = a.out.status ? a.out.status[cand] : (uint8_t)PDEVAL_CLS_ACCEPT;
-        // the reference checks the gradient (and Kerr the constant) before the point stage
-        const bool overridable = st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||
-                                 st == PDEVAL_CLS_REJECT_SYMBOLIC;
-        if ((s & 3) == P0_REJECT && overridable) {
-            write_point_reject(a, cand);
-            if (a.out.verdict_bits)
-                atomicAnd((uint32_t*)a.out.verdict_bits + (cand >> 5), ~(1u << (cand & 31)));
-        } else if ((s & 3) == P0_PASS && (s & P0_NZ) && st == PDEVAL_CLS_ACCEPT) {
-            nz_reject(a, cand);
+        uint8_t s = P0_NONE;
+        if (prog_bounds(a, cand, &beg, &end)) {
+            const int32_t* prog = a.ops + beg;
+            const uint32_t hdr = (uint32_t)prog[0];
+            // (the collect pass routes by depth)
+            if ((int)((hdr >> 8) & 0xffu) <= MAXD) s = dd_point_stage<PROB, T, MAXD>(a, cand, prog, (int)(end - beg), hdr, stk);
         }
-        a.pstate[cand] = (uint8_t)((a.pstate[cand] & ~(3 | P0_DD | P0_PROV | P0_NZ)) | s);
+        if constexpr (DEFER) {
+            a.ddps[cand] = s == P0_NONE ? kDdKeep : s;
+        } else {
+            if (s == P0_NONE) continue;   // not finite: keep the fp64 decision
+            dd_apply_one(a, cand, s);
+        }
+    }
+}
+
+// The early tier's classes, applied once the grid classes are final: the entries of the three
+// early lists (a.defer_list: real, a.cplx_list: complex, a.esc_list: real stack 3..8).
+template <int PROB>
+__global__ __launch_bounds__(256) void dd_apply_kernel(KernelArgs a) {
+    auto count = [&](const int32_t* c) { const int64_t v = *c; return v < a.list_capacity ? v : a.list_capacity; };
+    const int64_t n0 = count(a.defer_count);
+    const int64_t n1 = a.cplx_list ? count(a.cplx_count) : 0;
+    const int64_t n2 = count(a.esc_count);
+    for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < n0 + n1 + n2;
+         wi += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t cand = wi < n0 ? a.defer_list[wi] : (wi < n0 + n1 ? a.cplx_list[wi - n0] : a.esc_list[wi - n0 - n1]);
+        const uint8_t s = a.ddps[cand];
+        if (s != kDdKeep) dd_apply_one(a, cand, s);
     }
 }
 

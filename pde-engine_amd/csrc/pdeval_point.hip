@@ -16,17 +16,37 @@ void launch_point_list(int problem, int cplx, unsigned grid, hipStream_t s, cons
     }
 }
 
-void launch_dd_point(int problem, int kind, unsigned grid, hipStream_t s, const KernelArgs& a) {
+void launch_dd_point(int problem, int kind, unsigned grid, hipStream_t s, const KernelArgs& a, bool defer) {
     constexpr int FF = PDEVAL_PROBLEM_FORCE_FREE, KR = PDEVAL_PROBLEM_KERR;
     const size_t lds_ff = (size_t)nc(4) * 64 * sizeof(dd), lds_kr = (size_t)nc(2) * 64 * sizeof(dd);
+    constexpr int M8 = PDEVAL_MAX_STACK;
     if (problem == FF) {
-        if (kind == 0) hipLaunchKernelGGL((dd_point_kernel<FF, dd, 2>), dim3(grid), dim3(64), lds_ff, s, a);
-        else if (kind == 1) hipLaunchKernelGGL((dd_point_kernel<FF, dd, PDEVAL_MAX_STACK>), dim3(grid), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL((dd_point_kernel<FF, cdd, PDEVAL_MAX_STACK>), dim3(grid), dim3(64), 0, s, a);
+        if (kind == 0) {
+            if (defer) hipLaunchKernelGGL((dd_point_kernel<FF, dd, 2, true>), dim3(grid), dim3(64), lds_ff, s, a);
+            else hipLaunchKernelGGL((dd_point_kernel<FF, dd, 2>), dim3(grid), dim3(64), lds_ff, s, a);
+        } else if (kind == 1) {
+            if (defer) hipLaunchKernelGGL((dd_point_kernel<FF, dd, M8, true>), dim3(grid), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((dd_point_kernel<FF, dd, M8>), dim3(grid), dim3(64), 0, s, a);
+        } else {
+            if (defer) hipLaunchKernelGGL((dd_point_kernel<FF, cdd, M8, true>), dim3(grid), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((dd_point_kernel<FF, cdd, M8>), dim3(grid), dim3(64), 0, s, a);
+        }
     } else {
-        if (kind == 0) hipLaunchKernelGGL((dd_point_kernel<KR, dd, 2>), dim3(grid), dim3(64), lds_kr, s, a);
-        else if (kind == 1) hipLaunchKernelGGL((dd_point_kernel<KR, dd, PDEVAL_MAX_STACK>), dim3(grid), dim3(64), 0, s, a);
+        if (kind == 0) {
+            if (defer) hipLaunchKernelGGL((dd_point_kernel<KR, dd, 2, true>), dim3(grid), dim3(64), lds_kr, s, a);
+            else hipLaunchKernelGGL((dd_point_kernel<KR, dd, 2>), dim3(grid), dim3(64), lds_kr, s, a);
+        } else if (kind == 1) {
+            if (defer) hipLaunchKernelGGL((dd_point_kernel<KR, dd, M8, true>), dim3(grid), dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((dd_point_kernel<KR, dd, M8>), dim3(grid), dim3(64), 0, s, a);
+        }
     }
+}
+
+void launch_dd_apply(int problem, unsigned grid, hipStream_t s, const KernelArgs& a) {
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE)
+        hipLaunchKernelGGL((dd_apply_kernel<PDEVAL_PROBLEM_FORCE_FREE>), dim3(grid), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((dd_apply_kernel<PDEVAL_PROBLEM_KERR>), dim3(grid), dim3(256), 0, s, a);
 }
 
 void launch_point_eval(int problem, int tier, hipStream_t s, const KernelArgs& a, const int32_t* prog, int plen,

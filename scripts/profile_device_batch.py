@@ -27,7 +27,7 @@ def main():
     ops, off, _ = load_programs("force_free_d4_validated")
     rng = np.random.default_rng(0)
     perm = rng.permutation(len(off) - 1)
-    for env in ({}, {'PDEVAL_SORT': '0'}):
+    for env in ({}, {'PDEVAL_DD_EARLY': '0'}):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:

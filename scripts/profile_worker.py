@@ -38,6 +38,18 @@ def main():
         _results(c, p, t, locs, tagger); t4 = time.perf_counter()
         st['prepare'] += t1 - t0; st['device'] += t2 - t1; st['finish'] += t3 - t2; st['results'] += t4 - t3
     print('stage seconds (batch %d):' % b, {k: round(v, 4) for k, v in st.items()})
+    # the host steps and the tuples alone (what holds the GIL in the pipeline), by function
+    done = []
+    for k in range(0, len(items), b):
+        c = items[k:k + b]
+        p = bv.prepare_strings([s for _, s in c])
+        done.append((c, p, bv.run_prepared(p)))
+    pr = cProfile.Profile()
+    pr.enable()
+    for c, p, r in done:
+        _results(c, p, bv.finish(p, r), locs, tagger)
+    pr.disable()
+    pstats.Stats(pr).sort_stats('tottime').print_stats(25)
     # pipeline shapes (depth, compile threads), no profiler; the first is process_batches' default
     for depth, comp in ((8, 4), (12, 6), (16, 8)):
         t0 = time.perf_counter()
