@@ -409,9 +409,10 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
     process_batch(items[:batch], prob.validator, kw, locs, tagger)      # warm
     out = {'candidates': len(items), 'host_threads': host_threads()}
     t0 = time.perf_counter()
-    ref = []
+    ref, ref_batches = [], []
     for k in range(0, len(items), batch):
-        ref.extend(process_batch(items[k:k + batch], prob.validator, kw, locs, tagger))
+        ref_batches.append(process_batch(items[k:k + batch], prob.validator, kw, locs, tagger))
+        ref.extend(ref_batches[-1])
     dt = time.perf_counter() - t0
     out['process_batch'] = {'batch': batch, 'seconds': round(dt, 3), 'candidates_per_s': round(len(items) / dt),
                             'valid': sum(1 for t in ref if t[1]), 'paper_tagged': sum(1 for t in ref if t[3])}
@@ -424,6 +425,8 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
         dt = time.perf_counter() - t0
         out[f'pipelined_b{b}'] = {'seconds': round(dt, 3), 'candidates_per_s': round(len(items) / dt),
                                   'tuples_identical': got == ref}
+    for procs in (2, 3):
+        out[f'pool{procs}_b{batch}'] = worker_pool(ref_batches, len(items), batch, procs)
     sample = random.Random(0).sample(items, min(inline_n, len(items)))
     v = prob.validator
     t_parse = t_val = 0.0
@@ -445,10 +448,58 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
                               'validate_split_us': inline_split(v, sample[:500], locs)}
     # headline: the worker's default queue batch (validator_worker batch_size=4096); the
     # larger batches are detail.  Every pipelined run must give process_batch's tuples.
-    out['tuples_identical_all'] = all(out[k]['tuples_identical'] for k in out if k.startswith('pipelined'))
+    out['tuples_identical_all'] = all(out[k]['tuples_identical'] for k in out
+                                      if k.startswith('pipelined') or k.startswith('pool'))
+    # headline: the worker pool as the reference deploys it (--validators N processes), two
+    # processes on this one GPU at the queue's default batch, each taking every other batch;
+    # one process's pipeline (pipelined_b4096) and the larger batches are detail
     out['headline_batch'] = batch
-    out['candidates_per_s'] = out[f'pipelined_b{batch}']['candidates_per_s'] if out['tuples_identical_all'] else None
+    out['headline'] = f'pool2_b{batch}'
+    out['candidates_per_s'] = out[out['headline']]['candidates_per_s'] if out['tuples_identical_all'] else None
+    out['single_process_candidates_per_s'] = out[f'pipelined_b{batch}']['candidates_per_s']
     return out
+
+
+def worker_pool(ref_batches, n_items, batch, procs):
+    """N worker processes on one GPU (scripts/worker_child.py), the reference's --validators N
+    (general_method_paper_reproduction.py:802-823): each takes every N-th queue batch of the
+    same stream and runs process_batches; started as child processes (no exec in this one),
+    timed from a common start line to the last result.  Their result tuples are compared with
+    process_batch's, batch by batch (SHA-256 of each process's tuples in its own order)."""
+    import hashlib
+    import subprocess
+    script = os.path.join(ROOT, 'scripts', 'worker_child.py')
+    ps = [subprocess.Popen([sys.executable, script, '--part', str(k), '--parts', str(procs), '--batch', str(batch)],
+                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True) for k in range(procs)]
+    try:
+        for p in ps:
+            line = p.stdout.readline()
+            while line and line.strip() != 'READY':
+                line = p.stdout.readline()
+            if not line:
+                raise RuntimeError('worker_child exited before READY')
+        t0 = time.perf_counter()
+        for p in ps:
+            p.stdin.write('go\n')
+            p.stdin.flush()
+        res = [json.loads(p.stdout.readline()) for p in ps]
+        wall = time.perf_counter() - t0
+        for p in ps:
+            p.wait(timeout=120)
+    finally:
+        for p in ps:
+            if p.poll() is None:
+                p.kill()
+    same = True
+    for k, r in enumerate(res):
+        h = hashlib.sha256()
+        for rb in ref_batches[k::procs]:
+            h.update(repr(rb).encode())
+        same = same and h.hexdigest() == r['digest']
+    rows = sum(r['rows'] for r in res)
+    return {'processes': procs, 'rows': rows, 'seconds': round(wall, 3),
+            'candidates_per_s': round(rows / wall) if rows == n_items else None,
+            'per_process_s': [round(r['seconds'], 3) for r in res], 'tuples_identical': same}
 
 
 def inline_split(v, sample, locs):
