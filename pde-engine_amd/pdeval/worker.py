@@ -137,8 +137,10 @@ def validator_worker(run_id: str, table_name: Optional[str], db_path: Optional[s
                      problem_name: str = 'force_free', task_queue=None, result_queue=None,
                      batch_size: int = 4096, device: int = 0, idle_exit_s: Optional[float] = None,
                      local_workers: Optional[int] = None):
-    """Worker process body (one per GPU).  Returns the number of candidates validated.
-    ``local_workers``: GPU workers on this host (their SymPy pools share its cores)."""
+    """Worker process body (``--validators`` process; two per GPU keep the device busy, one
+    process's Python parts share a GIL: INTEGRATION.md §3).  Returns the number of candidates
+    validated.  ``local_workers``: worker processes on this host (their SymPy pools share its
+    cores)."""
     # the SymPy pool for declined strings and host checks, before the GPU is touched
     hostpool.start(local_workers=local_workers)
     try:
