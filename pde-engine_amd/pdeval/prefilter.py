@@ -140,10 +140,19 @@ def filter_one(args) -> Filtered:
     return Filtered(False, normalized, sig, const_only)
 
 
+class StreamResult(NamedTuple):
+    inserted: List[int]     # rows the driver inserts (not degenerate, key not seen before)
+    kept: List[int]         # of those, the ones that reach validate (not constant-only)
+    recs: List[Filtered]    # every candidate's record
+    stats: dict
+
+
 def filter_stream(slug: str, strings: Sequence[str], seen: Optional[set] = None,
-                  item_timeout: Optional[float] = None) -> Tuple[List[int], List[Filtered], dict]:
-    """The driver's filters over a stream (in stream order): returns the indices of the
-    candidates that reach ``validate``, every candidate's ``Filtered`` record, and counts.
+                  item_timeout: Optional[float] = None) -> StreamResult:
+    """The driver's filters over a stream (in stream order): the indices of the rows it
+    inserts into the run table and of those that reach ``validate`` (a constant-only row is
+    inserted and recorded as 'constant-only (skipped)', :1292-1294), every candidate's
+    ``Filtered`` record, and counts.
     ``seen``: the run table's keys so far (updated in place; a resumed run passes its table's
     ``normalized`` column).  The per-candidate work runs over the SymPy pool when it runs
     (``pdeval.hostpool``); ``item_timeout`` (the reference has none) keeps a candidate whose
@@ -155,6 +164,7 @@ def filter_stream(slug: str, strings: Sequence[str], seen: Optional[set] = None,
             for r, (_, s) in zip(recs, items)]
     seen = set() if seen is None else seen
     kept: List[int] = []
+    inserted: List[int] = []
     stats = {'streamed': len(strings), 'degenerate': 0, 'duplicate': 0, 'const_only': 0}
     for i, r in enumerate(recs):            # UNIQUE(normalized), in stream order
         if r.degenerate:
@@ -164,9 +174,10 @@ def filter_stream(slug: str, strings: Sequence[str], seen: Optional[set] = None,
             stats['duplicate'] += 1
             continue
         seen.add(r.normalized)
+        inserted.append(i)
         if r.const_only:
             stats['const_only'] += 1
             continue
         kept.append(i)
     stats['validated'] = len(kept)
-    return kept, recs, stats
+    return StreamResult(inserted, kept, recs, stats)

@@ -34,9 +34,11 @@ def test_stream_prefix_reaches_validate_as_in_reference(slug, n):
         rows = [l.rstrip('\n').split('\t') for l in f][:n]
     with gzip.open(os.path.join(G.GOLDEN, 'streams', f'{slug}_d3_validated.txt.gz'), 'rt') as f:
         ref = [int(l.split('\t')[0]) for l in f]
-    kept, recs, stats = F.filter_stream(slug, [r[1] for r in rows])
-    assert kept == [i for i in ref if i < n]
-    assert stats['validated'] + stats['degenerate'] + stats['duplicate'] + stats['const_only'] == n
+    res = F.filter_stream(slug, [r[1] for r in rows])
+    assert res.kept == [i for i in ref if i < n]
+    st = res.stats
+    assert st['validated'] + st['degenerate'] + st['duplicate'] + st['const_only'] == n
+    assert len(res.inserted) == st['validated'] + st['const_only'] and set(res.kept) <= set(res.inserted)
 
 
 def test_keys_equal_the_reference_run_table():
