@@ -158,6 +158,8 @@ typedef struct pdeval_params {
     double res_rel_acc;  /* point stage: a residual decided in fp64 must carry a
                             first-order error bound noise <= res_rel_acc x |res| (1e-11),
                             else it is re-evaluated in double-double  */
+    double omega2;       /* force-free: Omega^2 of rotating field lines, a constant
+                            (validator.py:326-329); 0 = the problem path's Omega = 0  */
 } pdeval_params;
 
 /* Per-candidate outputs; any pointer may be NULL (not produced).  Host or device memory

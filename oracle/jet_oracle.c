@@ -100,6 +100,10 @@ static void w_horner(const double* h0, const double* F, double* out, int K) {
 #define REXP exp
 #define RLOG log
 #define CI I
+/* force-free Omega^2 (pdeval_params.omega2), set by oracle_validate / oracle_set_omega2 */
+static double OM2 = 0.0;
+int oracle_set_omega2(double w) { OM2 = w; return 0; }
+
 #define S double
 #define FN(name) name##_r
 #include "jet_oracle_impl.h"
@@ -408,6 +412,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                     int64_t first, int64_t count) {
     double *px, *py;
     int nref;
+    if (prm) OM2 = problem == PDEVAL_PROBLEM_FORCE_FREE ? prm->omega2 : 0.0;
     int npts = build_points(problem, &px, &py, &nref);
     int G = npts - nref;
     int fp[PDEVAL_FP_N] = {0};

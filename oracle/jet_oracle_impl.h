@@ -320,7 +320,8 @@ static S FN(partial)(const S* c, int i, int j) {
     return c[IDX(i, j)] * (fct[i] * fct[j]);
 }
 
-/* Force-free determinant in closed form from partials (validator.py:323-347, Omega = 0).
+/* Force-free determinant in closed form from partials (validator.py:323-347; OM2 = Omega^2,
+ * 0 on the problem path).
  * mag != 0: every term replaced by its magnitude (the scale S). */
 static S FN(ff_det)(const S* c, CT rho, int mag) {
 #define M_(x) (mag ? (S)CABS(x) : (x))
@@ -345,6 +346,29 @@ static S FN(ff_det)(const S* c, CT rho, int mag) {
     S Brr = 2 * (u20 * u20 + p * u30 + u11 * u11 + q * u21);
     S Brz = 2 * (u11 * u20 + p * u21 + u02 * u11 + q * u12);
     S Bzz = 2 * (u11 * u11 + p * u12 + u02 * u02 + q * u03);
+    if (OM2 != 0) {
+        /* rotating field lines, constant Omega (validator.py:326-329): with w = Omega^2,
+         * A = A_0 - w C,  C = rho^2 (u20 + u02) + rho u10;  B = (1 - w rho^2) B_0 -- the
+         * partials of both written out (the device does it on jets, ff_rotate_A / _B) */
+        const CT w = (CT)OM2, x = rho, x2 = rho * rho;
+        S Cr = 2 * x * (u20 + u02) + x2 * (u30 + u12) + u10 + x * u20;
+        S Cz = x2 * (u21 + u03) + x * u11;
+        S Crr = 2 * (u20 + u02) + 4 * x * (u30 + u12) + x2 * (u40 + u22) + 2 * u20 + x * u30;
+        S Crz = 2 * x * (u21 + u03) + x2 * (u31 + u13) + u11 + x * u21;
+        S Czz = x2 * (u22 + u04) + x * u12;
+        Ar = SUB_(Ar, w * Cr);
+        Az = SUB_(Az, w * Cz);
+        Arr = SUB_(Arr, w * Crr);
+        Arz = SUB_(Arz, w * Crz);
+        Azz = SUB_(Azz, w * Czz);
+        const S B0 = p * p + q * q;
+        S Brr2 = SUB_(Brr, w * (2 * B0 + 4 * x * Br + x2 * Brr));
+        S Brz2 = SUB_(Brz, w * (2 * x * Bz + x2 * Brz));
+        S Bzz2 = SUB_(Bzz, w * (x2 * Bzz));
+        S Br2 = SUB_(Br, w * (2 * x * B0 + x2 * Br));
+        S Bz2 = SUB_(Bz, w * (x2 * Bz));
+        Br = Br2; Bz = Bz2; Brr = Brr2; Brz = Brz2; Bzz = Bzz2;
+    }
     /* L_T f = q f_r - p f_z;  L_T^2 f = q (L_T f)_r - p (L_T f)_z */
     S LA = SUB_(q * Ar, p * Az), LB = SUB_(q * Br, p * Bz);
     S LAr = SUB_(u11 * Ar + q * Arr, u20 * Az + p * Arz);

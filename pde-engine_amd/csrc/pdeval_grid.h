@@ -742,7 +742,10 @@ template <int PROB, int MAXD, class T = double> constexpr size_t grid_lds(int wa
 // launches, as tier 2's parts do) and the part that completes the candidate writes the
 // outputs and zeroes the accumulator.  Sums of counts and the max of maxima do not depend on
 // the split, so the outputs are those of one wave.
-template <int PROB, int MAXD, class T = double>
+// ROT: the rotating force-free constraint (params.omega2 != 0, FFEpi::rotate_A / _B) -- its own
+// kernel instances, so the Omega = 0 epilogue compiles to the code it was (a runtime branch there
+// cost pass 1 20 %: 161.4 vs 133.7 ms, profiles/r04_o_ff.log)
+template <int PROB, int MAXD, class T = double, bool ROT = false>
 __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int lane, T* stk,
                                           int64_t* slow_list, int32_t* slow_count, int part = 0,
                                           int parts = 1) {
@@ -834,7 +837,8 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 const int base = a.n_ref + (row + q) * a.ny + sl * 64;   // point index of lane 0
                 PointResult r;
                 if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE)
-                    r = PD_EPI_TABLE_RCP ? ff_epilogue_r<T>(u[q].c, inv_x[q]) : ff_epilogue<T>(u[q].c, x[q]);
+                    r = PD_EPI_TABLE_RCP ? ff_epilogue_r<T>(u[q].c, inv_x[q], x[q], ROT ? a.prm.omega2 : 0.0)
+                                         : ff_epilogue<T>(u[q].c, x[q], ROT ? a.prm.omega2 : 0.0);
                 else r = kerr_epilogue<T>(u[q].c, kv[q]);
                 const double qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
                 if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {
@@ -907,7 +911,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
 #endif
 // SPLIT: the small-batch instance (grid_body's parts); the full-batch instance has parts == 1
 // folded in, so its code is the one-wave-per-candidate kernel
-template <int PROB, bool SPLIT>
+template <int PROB, bool SPLIT, bool ROT = false>
 __global__ __launch_bounds__(64 * PD_GRID_WPB, PROB == PDEVAL_PROBLEM_FORCE_FREE ? PD_GRID_WAVES_PER_SIMD : PD_KERR_WAVES_PER_SIMD)
 void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count, int parts_arg) {
     const int parts = SPLIT ? parts_arg : 1;
@@ -937,11 +941,11 @@ void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count, int part
     }
     if (wi >= a.n) return;
     const int64_t cand = (PD_GRID_PERM && a.perm) ? (int64_t)__builtin_amdgcn_readfirstlane(a.perm[wi]) : wi;
-    grid_body<PROB, 2>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, part, parts);
+    grid_body<PROB, 2, double, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, part, parts);
 }
 
 // pass 2: the stack-3 list a.list (count *a.list_count), persistent 64-thread blocks
-template <int PROB, bool SPLIT>
+template <int PROB, bool SPLIT, bool ROT = false>
 __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST_WAVES_PER_SIMD) void grid_list_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count, int parts_arg) {
     const int parts = SPLIT ? parts_arg : 1;
 #ifndef PD_HOST_SIM
@@ -955,7 +959,7 @@ __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST
     for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
         const int64_t wi = wp / parts;
         const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
-        grid_body<PROB, 3>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, (int)(wp % parts), parts);
+        grid_body<PROB, 3, double, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, (int)(wp % parts), parts);
     }
 }
 
@@ -965,7 +969,7 @@ __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST
 #ifndef PD_CPLX_WAVES_PER_SIMD
 #define PD_CPLX_WAVES_PER_SIMD 2
 #endif
-template <bool SPLIT>
+template <bool SPLIT, bool ROT = false>
 __global__ __launch_bounds__(64, PD_CPLX_WAVES_PER_SIMD) void grid_cplx_kernel(KernelArgs a, int64_t* slow_list,
                                                                                 int32_t* slow_count, int parts_arg) {
     const int parts = SPLIT ? parts_arg : 1;
@@ -980,7 +984,7 @@ __global__ __launch_bounds__(64, PD_CPLX_WAVES_PER_SIMD) void grid_cplx_kernel(K
     for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
         const int64_t wi = wp / parts;
         const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
-        grid_body<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count,
+        grid_body<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count,
                                                       (int)(wp % parts), parts);
     }
 }

@@ -21,7 +21,10 @@ void launch_grid(int problem, int64_t n, hipStream_t s, const KernelArgs& a,
     const unsigned blocks = (unsigned)((n * parts + PD_GRID_WPB - 1) / PD_GRID_WPB);
     const size_t lff = grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2>(PD_GRID_WPB), lk = grid_lds<PDEVAL_PROBLEM_KERR, 2>(PD_GRID_WPB);
     if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
-        if (parts > 1)
+        if (a.prm.omega2 != 0.0)   // rotating field lines: the ROT instance (any parts)
+            hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE, true, true>), dim3(blocks), dim3(64 * PD_GRID_WPB),
+                               lff, s, a, slow_list, slow_count, parts);
+        else if (parts > 1)
             hipLaunchKernelGGL((grid_kernel<PDEVAL_PROBLEM_FORCE_FREE, true>), dim3(blocks), dim3(64 * PD_GRID_WPB), lff,
                                s, a, slow_list, slow_count, parts);
         else
@@ -60,7 +63,9 @@ void launch_decode(int problem, int64_t n, hipStream_t s, const KernelArgs& a) {
 void launch_grid_cplx(unsigned blocks, hipStream_t s, const KernelArgs& a, int64_t* slow_list, int32_t* slow_count,
                       int parts) {
     const size_t l = grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx>(1);
-    if (parts > 1)
+    if (a.prm.omega2 != 0.0)
+        hipLaunchKernelGGL((grid_cplx_kernel<true, true>), dim3(blocks), dim3(64), l, s, a, slow_list, slow_count, parts);
+    else if (parts > 1)
         hipLaunchKernelGGL(grid_cplx_kernel<true>, dim3(blocks), dim3(64), l, s, a, slow_list, slow_count, parts);
     else
         hipLaunchKernelGGL(grid_cplx_kernel<false>, dim3(blocks), dim3(64), l, s, a, slow_list, slow_count, 1);
@@ -70,7 +75,10 @@ void launch_grid_list(int problem, unsigned blocks, hipStream_t s, const KernelA
                       int64_t* slow_list, int32_t* slow_count, int parts) {
     const size_t lff = grid_lds<PDEVAL_PROBLEM_FORCE_FREE, 3>(1), lk = grid_lds<PDEVAL_PROBLEM_KERR, 3>(1);
     if (problem == PDEVAL_PROBLEM_FORCE_FREE) {
-        if (parts > 1)
+        if (a.prm.omega2 != 0.0)
+            hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_FORCE_FREE, true, true>), dim3(blocks), dim3(64), lff, s,
+                               a, slow_list, slow_count, parts);
+        else if (parts > 1)
             hipLaunchKernelGGL((grid_list_kernel<PDEVAL_PROBLEM_FORCE_FREE, true>), dim3(blocks), dim3(64), lff, s, a,
                                slow_list, slow_count, parts);
         else

@@ -546,6 +546,10 @@ struct PointResult {
 // p = u_rho, q = u_z (order 3);  A = p_rho + q_z - p/rho,  B = p^2 + q^2 (order 2);
 // LA = q A_rho - p A_z, LB = q B_rho - p B_z (order 1);  L2A = q LA_rho - p LA_z (order 0);
 // det = LA * L2B - LB * L2A.   (validator.py:323-347; Omega = 0 on the problem path)
+// Rotating field lines, a constant Omega (validator.py:326-329, om2 = Omega^2 != 0):
+// A = (1 - rho^2 om2)(u_rr + u_zz) - (1 + rho^2 om2)/rho u_r = A_0 - om2 (rho^2 (u_rr + u_zz) + rho u_r)
+// and B = (1 - rho^2 om2) B_0: corrections of A_0 and B_0 in ff_rotate_A / _B, out of line
+// behind a uniform branch, so the Omega = 0 epilogue is the same code as before.
 // MAG = true evaluates the same expression on magnitudes with every difference turned into
 // a sum: S >= sum of |monomials| of the fully expanded determinant.
 template <class T, bool MAG> struct FFEpi {
@@ -577,8 +581,9 @@ template <class T, bool MAG> struct FFEpi {
 
     // rho: R = double, or dd in the double-double point tier; r0 = rcp(rho) (the grid passes
     // pass their row's correctly rounded 1/x from the host table, the same value)
-    template <class R> static PD_HD T eval(const T* u, R rho) { return eval_r(u, rcp(rho)); }
-    template <class R> static PD_HD T eval_r(const T* u, R r0) {
+    template <class R> static PD_HD T eval(const T* u, R rho, double om2 = 0.0) { return eval_r(u, rcp(rho), rho, om2); }
+    template <class R> static PD_HD T eval_r(const T* u, R r0) { return eval_r(u, r0, r0, 0.0); }
+    template <class R> static PD_HD T eval_r(const T* u, R r0, R rho, double om2) {
         // 1/rho jet in the rho direction: (-1)^i / rho^(i+1)
         const R ri[3] = {r0, r0 * r0 * (MAG ? 1.0 : -1.0), r0 * r0 * r0};
         T LA[3], LB[3];
@@ -597,6 +602,7 @@ template <class T, bool MAG> struct FFEpi {
                     for (int i1 = 1; i1 <= i; ++i1) pr = fmac(P(u, i - i1, j), cvt<T>(ri[i1]), pr);
                     A[ji(i, j)] = s + sgn(pr);
                 }
+            if (om2 != 0.0) rotate_A(A, u, rho, om2);
             lie1(u, A, LA);
         }
         {
@@ -619,6 +625,7 @@ template <class T, bool MAG> struct FFEpi {
                         }
                     B[ji(i, j)] = s;
                 }
+            if (om2 != 0.0) rotate_B(B, rho, om2);
             lie1(u, B, LB);
         }
         // L_T^2 f (order 0) = q (L_T f)_rho - p (L_T f)_z
@@ -628,11 +635,55 @@ template <class T, bool MAG> struct FFEpi {
         // det[[L_T A, L_T B], [L_T^2 A, L_T^2 B]]   (validator.py:347)
         return LA[0] * L2B + sgn(LB[0] * L2A);
     }
+
+    // A -= om2 C, C = rho^2 (u_rr + u_zz) + rho u_r, order 2 in (rho, z); the rho^k factors as
+    // jets in the rho direction: rho = (x, 1), rho^2 = (x^2, 2x, 1)
+    template <class R> static PD_HD void rotate_A(T* A, const T* u, R x, double om2) {
+        T PQ[6];
+#pragma unroll
+        for (int d = 0; d <= 2; ++d)
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                const int i = d - j;
+                PQ[ji(i, j)] = fmac(U(u, i, j + 2), from_real<T>((double)((j + 1) * (j + 2))),
+                                    U(u, i + 2, j) * (double)((i + 1) * (i + 2)));
+            }
+        const T x1 = cvt<T>(x), x2 = cvt<T>(x * x), x2t = cvt<T>(x + x);
+#pragma unroll
+        for (int d = 0; d <= 2; ++d)
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                const int i = d - j;
+                T c = x2 * PQ[ji(i, j)];
+                c = fmac(x1, P(u, i, j), c);
+                if (i >= 1) c = c + fmac(x2t, PQ[ji(i - 1, j)], P(u, i - 1, j));
+                if (i >= 2) c = c + PQ[ji(i - 2, j)];
+                A[ji(i, j)] = A[ji(i, j)] + sgn(c * om2);
+            }
+    }
+    // B (1 - om2 rho^2)
+    template <class R> static PD_HD void rotate_B(T* B, R x, double om2) {
+        T B0[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) B0[k] = B[k];
+        const T x2 = cvt<T>(x * x), x2t = cvt<T>(x + x);
+#pragma unroll
+        for (int d = 0; d <= 2; ++d)
+#pragma unroll
+            for (int j = 0; j <= d; ++j) {
+                const int i = d - j;
+                T c = x2 * B0[ji(i, j)];
+                if (i >= 1) c = fmac(x2t, B0[ji(i - 1, j)], c);
+                if (i >= 2) c = c + B0[ji(i - 2, j)];
+                B[ji(i, j)] = B0[ji(i, j)] + sgn(c * om2);
+            }
+    }
 };
 
 // (inv_rho = rcp(rho): the lean grid passes read it from the grid's reciprocal table instead of
 // dividing once per row; ff_epilogue below divides)
-template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T* u, double inv_rho) {
+template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T* u, double inv_rho, double rho = 0.0,
+                                                                       double om2 = 0.0) {
     PointResult r;
 #ifdef PD_VAR_NO_EPI   // timing variant: no determinant at all (verdicts meaningless)
     {
@@ -645,7 +696,7 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T*
         return r;
     }
 #endif
-    const T det = FFEpi<T, false>::eval_r(u, inv_rho);
+    const T det = FFEpi<T, false>::eval_r(u, inv_rho, rho, om2);
     // keep the signed and the magnitude evaluations apart: interleaved, the scheduler keeps
     // both sets of intermediates live
     __builtin_amdgcn_sched_barrier(0);
@@ -657,9 +708,9 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T*
         double m[15];
 #pragma unroll
         for (int i = 0; i < 15; ++i) m[i] = mag(u[i]);
-        S = FFEpi<double, true>::eval_r(m, inv_rho);
+        S = FFEpi<double, true>::eval_r(m, inv_rho, rho, om2);
     } else {
-        S = FFEpi<double, true>::eval_r(u, inv_rho);
+        S = FFEpi<double, true>::eval_r(u, inv_rho, rho, om2);
     }
 #endif
     r.res_abs = mag(det);
@@ -679,8 +730,8 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T*
     return r;
 }
 
-template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u, double rho) {
-    return ff_epilogue_r<T>(u, rcp(rho));
+template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u, double rho, double om2 = 0.0) {
+    return ff_epilogue_r<T>(u, rcp(rho), rho, om2);
 }
 
 // Kerr surrogate: L[u] = k1 u_rr + k2 u_xx + k3 u_r + k4 u_x, coefficients per point.
@@ -1034,7 +1085,7 @@ void validate_kernel(KernelArgs a) {
             if (rc == RUN_UNSUPPORTED) { status = PDEVAL_CLS_UNSUPPORTED; break; }
             if (rc == RUN_BAD) { status = PDEVAL_CLS_BAD_PROGRAM; break; }
             PointResult r;
-            if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x);
+            if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x, a.prm.omega2);
             else r = kerr_epilogue<T>(u.c, a.kc + 4 * pp);
             const double qv = scaled(r.res_abs, r.scale);
             if (active) {

@@ -111,8 +111,8 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
     const double* kc = a.kc ? a.kc + 4 * k : nullptr;
     T res;
     if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-        res = FFEpi<T, false>::eval(u.c, x);
-        r.S = FFEpi<double, true>::eval(m, hi_of(x));
+        res = FFEpi<T, false>::eval(u.c, x, a.prm.omega2);
+        r.S = FFEpi<double, true>::eval(m, hi_of(x), a.prm.omega2);
     } else {
         if constexpr (std::is_same<V, dd>::value) {
             dd kcd[4];
@@ -122,7 +122,7 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
         else res = kerr_lhs<T, double>(u.c, kc, &r.S);
     }
     const double unit = std::is_same<V, dd>::value ? dd_unit() / kEps : 1.0;
-    r.noise = residual_noise<PROB, T>(u.c, e, hi_of(x), kc, r.S) * unit;
+    r.noise = residual_noise<PROB, T>(u.c, e, hi_of(x), kc, r.S, a.prm.omega2) * unit;
     r.res_re = re_hi(res);
     r.res_im = im_hi(res);
     r.res_abs = mag(res);
@@ -576,8 +576,8 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
         T res;
         double S;
         if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-            res = FFEpi<T, false>::eval(u.c, x);
-            S = FFEpi<double, true>::eval(m, x.hi);
+            res = FFEpi<T, false>::eval(u.c, x, a.prm.omega2);
+            S = FFEpi<double, true>::eval(m, x.hi, a.prm.omega2);
         } else {
             dd kc[4];
             kc_ref_at(a, p, kc);

@@ -426,13 +426,13 @@ template <class T, int K, int MAXD, class V = double> struct ErrInterp {
 // First-order rounding-noise bound of the residual at one point.
 template <int PROB, class T> __device__ __forceinline__ double residual_noise(const T* u, const double* e,
                                                                               double x, const double* kc,
-                                                                              double S) {
+                                                                              double S, double om2) {
     constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
     double up[nc(K)];
 #pragma unroll
     for (int i = 0; i < nc(K); ++i) up[i] = mag(u[i]) + kNoiseGamma * e[i];
     double S2;
-    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) S2 = FFEpi<double, true>::eval(up, x);
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) S2 = FFEpi<double, true>::eval(up, x, om2);
     else S2 = kerr_epilogue<double>(up, kc).scale;
     return (S2 - S) * (kEps / kNoiseGamma) + kEps * S;
 }
@@ -499,13 +499,13 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             if (rc == RUN_OK) {
                 const double* kc = a.kc ? a.kc + 4 * l : nullptr;
                 PointResult r;
-                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x);
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x, a.prm.omega2);
                 else r = kerr_epilogue<T>(u.c, kc);
                 bool fails;
                 if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) fails = !(scaled(r.res_abs, r.scale) <= a.prm.tau_point);
                 else fails = !(r.res_abs < a.prm.kerr_abs_tol);
                 if (!r.finite) real_fail = true;
-                else if (fails) real_fail = r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale);
+                else if (fails) real_fail = r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale, a.prm.omega2);
             }
             point_reject = __any(active && real_fail);
             if (point_reject) continue;     // confirmed: pass 1's REJECT_POINT stands
@@ -531,7 +531,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
                 if (rc != RUN_OK) { ++nnonfin; continue; }
                 const double* kc = a.kc ? a.kc + 4 * p : nullptr;
                 PointResult r;
-                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x);
+                if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<T>(u.c, x, a.prm.omega2);
                 else r = kerr_epilogue<T>(u.c, kc);
                 if (!r.finite) { ++nnonfin; continue; }
                 ++nfin;
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
                 if (!r.grad_zero) grad_nz = true;
                 if (qv > a.prm.tau_grid) {
                     ++nb1;
-                    if (r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale)) ++nb2;
+                    if (r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale, a.prm.omega2)) ++nb2;
                 }
             }
             nb1 = wave_sum(nb1);
@@ -642,12 +642,12 @@ __global__ __launch_bounds__(64, 1) void eval_points_kernel(const int32_t* prog,
                          : I::run(prog, 1, plen, x, y, u, vs, lane, P);
     PointResult r;
     const double* k4 = kc ? kc + 4 * pc : nullptr;
-    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r = ff_epilogue<double>(u.c, x);   // (Omega = 0)
     else r = kerr_epilogue<double>(u.c, k4);
     if (p < npts) {
         out[4 * p + 0] = rc ? NAN : r.res_abs;
         out[4 * p + 1] = rc ? NAN : r.scale;
-        out[4 * p + 2] = (rc || !tier2) ? 0.0 : residual_noise<PROB, double>(u.c, e, x, k4, r.scale);
+        out[4 * p + 2] = (rc || !tier2) ? 0.0 : residual_noise<PROB, double>(u.c, e, x, k4, r.scale, 0.0);
         out[4 * p + 3] = rc ? -1.0 : (r.finite ? 1.0 : 0.0);
         if (jets) {
 #pragma unroll

@@ -473,7 +473,7 @@ SYMBOLIC_TIMEOUT_S = 60.0    # per candidate: the limit the reference fixtures w
 
 
 def symbolic_stage(pd, items, out, mode: str = 'text', timeout: float = SYMBOLIC_TIMEOUT_S,
-                   kerr=None) -> List[int]:
+                   kerr=None, omega: str = '0') -> List[int]:
     """Force-free: the reference's symbolic stage replayed on the host (pdeval.symbolic) where
     it decides the verdict or the text (``problems/force_free/validator.py:404-427``):
 
@@ -509,11 +509,12 @@ def symbolic_stage(pd, items, out, mode: str = 'text', timeout: float = SYMBOLIC
     # reject (det not zero) and, in 'text' mode, a structural-rule reject take the branch text
     def need_verdict(c):
         return mode == 'replay' and c != CLS_REJECT_GRID
-    args = [(pd.slug, items[i] if isinstance(items[i], str) else None, need_verdict(int(st[i]))) for i in sel]
+    args = [(pd.slug, items[i] if isinstance(items[i], str) else None, need_verdict(int(st[i])), omega) for i in sel]
     if all(a[1] is not None for a in args):
         res = hostpool.run(S.replay_str, args, min_items=1, item_timeout=timeout, default=None)
     else:
-        res = [hostpool._call_bounded(lambda it: S.ff_replay(it[0], pd.x, pd.y, it[1]),
+        om = sp.sympify(omega)
+        res = [hostpool._call_bounded(lambda it: S.ff_replay(it[0], pd.x, pd.y, it[1], om),
                              (items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i]),
                               need_verdict(int(st[i]))), timeout, None) for i in sel]
     ov = out.setdefault('reason_override', {})
@@ -580,13 +581,18 @@ class BatchValidator:
     text) or 'replay' (the reference's symbolic verdicts too)."""
 
     def __init__(self, problem: str = 'force_free', device: int = 0, params=None, kerr=None,
-                 symbolic: str = 'off', symbolic_timeout: float = SYMBOLIC_TIMEOUT_S):
+                 symbolic: str = 'off', symbolic_timeout: float = SYMBOLIC_TIMEOUT_S, omega: str = '0'):
         from ._lib import Context, default_params, default_kerr_constants
         self.pd = P.get(problem)
         self.device = device
         self.kerr = kerr if kerr is not None or self.pd.problem_id != PROBLEM_KERR else default_kerr_constants()
         self.ctx = Context(self.pd.problem_id, device=device, kerr=kerr)
         self.params = params if params is not None else default_params(self.pd.problem_id)
+        # force-free, rotating field lines: Omega (a constant, as a string of an exact number
+        # whose square is a double: omega2_value) -> params.omega2 (validator.py:326-329)
+        self.omega = omega
+        if self.pd.problem_id == PROBLEM_FORCE_FREE:
+            self.params.omega2 = omega2_value(omega)
         if symbolic not in SYMBOLIC_MODES:
             raise ValueError(f'symbolic mode {symbolic!r}: one of {SYMBOLIC_MODES}')
         self.symbolic = symbolic
@@ -626,7 +632,8 @@ class BatchValidator:
         mode = self.symbolic if symbolic is None else symbolic
         if mode != 'off' and (self.params.full_grid or self.problem_id == PROBLEM_KERR):
             symbolic_stage(self.pd, items, r, mode,
-                           self.symbolic_timeout if symbolic_timeout is None else symbolic_timeout, self.kerr)
+                           self.symbolic_timeout if symbolic_timeout is None else symbolic_timeout, self.kerr,
+                           omega=self.omega)
         return r
 
     def table(self, r, ops, off, notes) -> dict:
@@ -688,11 +695,26 @@ _VALIDATORS: Dict[tuple, BatchValidator] = {}
 _VLOCK = threading.Lock()
 
 
-def get_validator(problem: str, device: int = 0, kerr=None) -> BatchValidator:
-    """Process-wide BatchValidator per (problem, device, Kerr constants): one libpdeval context
-    per GPU and parameter set.  (The symbolic host mode is chosen per call by the plugins.)"""
-    key = (P.get(problem).slug, device, kerr.key() if kerr is not None else None)
+def omega2_value(omega) -> float:
+    """Omega**2 of the force-free rotating constraint as a double, exact (so the device's
+    Omega^2 is the reference's): Omega a constant whose square is a rational representable in
+    double precision (1, 2, 1/2, sqrt(2), ...).  A symbolic Omega (the reference allows a
+    function of u, validator.py:45) or an inexact square raises NotImplementedError."""
+    w = sp.sympify(omega)
+    if w.free_symbols:
+        raise NotImplementedError(f'Omega = {omega!r}: only a constant Omega is implemented')
+    w2 = sp.nsimplify(w ** 2, rational=True)
+    if not w2.is_Rational or sp.Rational(float(w2)) != w2:
+        raise NotImplementedError(f'Omega = {omega!r}: Omega**2 must be exact in double precision')
+    return float(w2)
+
+
+def get_validator(problem: str, device: int = 0, kerr=None, omega: str = '0') -> BatchValidator:
+    """Process-wide BatchValidator per (problem, device, Kerr constants, force-free Omega): one
+    libpdeval context per GPU and parameter set.  (The symbolic host mode is chosen per call by
+    the plugins.)"""
+    key = (P.get(problem).slug, device, kerr.key() if kerr is not None else None, str(omega))
     with _VLOCK:
         if key not in _VALIDATORS:
-            _VALIDATORS[key] = BatchValidator(problem, device, kerr=kerr)
+            _VALIDATORS[key] = BatchValidator(problem, device, kerr=kerr, omega=str(omega))
         return _VALIDATORS[key]

@@ -58,15 +58,19 @@ TEXT_EXPAND_FAIL = 'Invalid (expanded det != 0)'
 TEXT_EXPAND_ERR = 'Could not simplify det symbolically'
 
 
-def ff_det(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol) -> Optional[sp.Basic]:
-    """SymPy's det_M for u, built in the reference's order (validator.py:305-347; Omega = 0);
-    None for a zero gradient (the reference stops there)."""
+def ff_det(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol, Omega: sp.Basic = sp.Integer(0)) -> Optional[sp.Basic]:
+    """SymPy's det_M for u, built in the reference's order (validator.py:305-347, the rotating
+    form :326-329 when Omega != 0); None for a zero gradient (the reference stops there)."""
     u_r = u.diff(rho)
     u_z = u.diff(z)
     if u_r == 0 and u_z == 0:
         return None
-    A = u_r.diff(rho) + u_z.diff(z) - u_r / rho
-    B = u_r**2 + u_z**2
+    if Omega != 0:
+        A = (1 - rho**2 * Omega**2) * (u_r.diff(rho) + u_z.diff(z)) - (1 + rho**2 * Omega**2) / rho * u_r
+        B = (1 - rho**2 * Omega**2) * (u_r**2 + u_z**2)
+    else:
+        A = u_r.diff(rho) + u_z.diff(z) - u_r / rho
+        B = u_r**2 + u_z**2
 
     def lie(f):
         return u_z * f.diff(rho) - u_r * f.diff(z)
@@ -129,11 +133,12 @@ def ff_symbolic_stage(det_M: sp.Basic, verdict: bool = True) -> Tuple[bool, str]
         return False, TEXT_EXPAND_ERR
 
 
-def ff_replay(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol, verdict: bool = True) -> Optional[Tuple[bool, str]]:
+def ff_replay(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol, verdict: bool = True,
+              Omega: sp.Basic = sp.Integer(0)) -> Optional[Tuple[bool, str]]:
     """(ok, reason) of the reference's symbolic stage for a candidate that passed its point
     stage; None if SymPy fails (the device's verdict stands)."""
     try:
-        det_M = ff_det(u, rho, z)
+        det_M = ff_det(u, rho, z, Omega)
         if det_M is None:
             return None
         return ff_symbolic_stage(det_M, verdict)
@@ -171,9 +176,10 @@ _PDS: Dict[str, object] = {}
 
 def replay_str(args) -> Optional[Tuple[bool, str]]:
     """ff_replay of a candidate string, in a SymPy pool process (pdeval.hostpool.run):
-    ``(slug, expr_str, verdict)``; parsed with the driver's sympify locals
+    ``(slug, expr_str, verdict[, Omega])``; parsed with the driver's sympify locals
     (general_method_paper_reproduction.py:84-93)."""
-    slug, s, verdict = args
+    slug, s, verdict = args[:3]
+    omega = sp.sympify(args[3]) if len(args) > 3 else sp.Integer(0)
     from . import problem_defs as P
     if slug not in _PDS:
         _PDS[slug] = P.get(slug)
@@ -182,7 +188,7 @@ def replay_str(args) -> Optional[Tuple[bool, str]]:
         u = pd.parse(s)
     except Exception:   # noqa: BLE001
         return None
-    return ff_replay(u, pd.x, pd.y, verdict)
+    return ff_replay(u, pd.x, pd.y, verdict, omega)
 
 
 # ------------------------------------------------------------------ Kerr (text mode)

@@ -12,7 +12,10 @@ Differences, all deliberate:
   §4); an in-memory memo keyed by ``str(u)`` is kept instead;
 * ``fast_point_only=True`` returns the point-stage verdict ("Valid foliation (point check = 0)")
   -- the reference's fast branch fails on its own symbolic stand-ins (``:298-303, :323``);
-* ``Omega`` must be 0 (the problem path, ``problems/__init__.py:83``);
+* ``Omega``: 0 on the problem path (``problems/__init__.py:83``); a constant Omega != 0 (the
+  rotating constraint, ``:326-329``) is evaluated on the device too (``params.omega2``, the
+  rotation terms of ``FFEpi``), for any constant Omega whose square is an exact double (1, 2,
+  1/2, sqrt(2), ...); an Omega that is a function of u raises NotImplementedError;
 * ``symbolic`` chooses how much of the reference's symbolic stage (``:404-427``) is replayed
   on the host in SymPy (``pdeval.symbolic``): ``'off'`` (default: the device's verdicts, and
   the Lean text for every grid reject), ``'text'`` (grid rejects get the reference's branch
@@ -33,9 +36,10 @@ import sympy as sp
 class PreciseFoliationValidator:
     def __init__(self, cache_db: Optional[str] = None, use_lean: bool = True, Omega: Any = 0,
                  device: int = 0, symbolic: Optional[str] = None, symbolic_timeout: float = 60.0):
+        from pdeval.batch import SYMBOLIC_MODES, omega2_value
         if Omega != 0:
-            raise NotImplementedError('only the non-rotating constraint (Omega = 0) is implemented')
-        from pdeval.batch import SYMBOLIC_MODES
+            omega2_value(Omega)     # a constant whose square is exact, else NotImplementedError
+        self._omega_key = '0' if Omega == 0 else str(sp.nsimplify(sp.sympify(Omega)))
         self.symbolic = symbolic or os.environ.get('PDEVAL_SYMBOLIC', 'off')
         if self.symbolic not in SYMBOLIC_MODES:
             raise ValueError(f'symbolic mode {self.symbolic!r}: one of {SYMBOLIC_MODES}')
@@ -53,7 +57,7 @@ class PreciseFoliationValidator:
     def _validator(self):
         if self._bv is None:
             from pdeval.batch import get_validator
-            self._bv = get_validator('force_free', self.device)
+            self._bv = get_validator('force_free', self.device, omega=self._omega_key)
         return self._bv
 
     def _canon(self, u: sp.Basic) -> sp.Basic:

@@ -44,7 +44,7 @@ def _alarm(_sig, _frm):
     raise _Timeout()
 
 
-def _init_worker(ref, problem, kerr_a_value='1/10', kerr_op_a_zero=False):
+def _init_worker(ref, problem, kerr_a_value='1/10', kerr_op_a_zero=False, ff_omega='0'):
     global _D
     os.chdir(ref)
     sys.path.insert(0, ref)
@@ -54,7 +54,8 @@ def _init_worker(ref, problem, kerr_a_value='1/10', kerr_op_a_zero=False):
     d = GeneralFoliationDiscovery(use_lean_normalizer=True, problem_name=problem, mode='parallel')
     if d.problem.slug == 'force_free':
         from problems.force_free.validator import PreciseFoliationValidator
-        v = PreciseFoliationValidator(cache_db=':memory:', use_lean=False)
+        # (a fixture run may pass a non-zero Omega, validator.py:38-49: the rotating constraint)
+        v = PreciseFoliationValidator(cache_db=':memory:', use_lean=False, Omega=sp.sympify(ff_omega))
         v.use_lean = True
         v.lean_normalizer = LeanNormalizer(cache_db=':memory:')
     else:
@@ -176,6 +177,7 @@ def main():
     ap.add_argument('--timeout', type=int, default=60)
     ap.add_argument('--procs', type=int, default=os.cpu_count())
     ap.add_argument('--kerr-a-value', default='1/10', help="Kerr validator's a_value")
+    ap.add_argument('--ff-omega', default='0', help="force-free validator's Omega (a constant)")
     ap.add_argument('--kerr-op-a-zero', action='store_true',
                     help='Kerr operator built with a = 0 (validator a argument = the number 0)')
     a = ap.parse_args()
@@ -225,7 +227,7 @@ def main():
         items = [it for it in items if it[1] == a.depth]
     if a.sample and a.sample < len(items):
         items = sorted(random.Random(a.seed).sample(items, a.sample))
-    init = (a.ref, a.problem, a.kerr_a_value, a.kerr_op_a_zero)
+    init = (a.ref, a.problem, a.kerr_a_value, a.kerr_op_a_zero, a.ff_omega)
     with mp.get_context('fork').Pool(a.procs, _init_worker, init,
                                      maxtasksperchild=200) as pool, open(a.out, 'w') as f:
         n = 0
@@ -235,6 +237,8 @@ def main():
                 rec['limit_s'] = a.timeout
             if a.problem != 'force_free' and (a.kerr_a_value != '1/10' or a.kerr_op_a_zero):
                 rec['kerr'] = {'M_value': '1', 'a_value': a.kerr_a_value, 'op_a_zero': a.kerr_op_a_zero}
+            if a.problem == 'force_free' and a.ff_omega != '0':
+                rec['omega'] = a.ff_omega
             f.write(json.dumps(rec) + '\n')
             f.flush()
             n += 1

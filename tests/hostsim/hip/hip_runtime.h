@@ -11,6 +11,7 @@
 #define __device__
 #define __global__
 #define __forceinline__ inline
+#define __noinline__ __attribute__((noinline))
 #define __launch_bounds__(...)
 #define __shared__
 struct pd_dim3 { unsigned x = 0, y = 0, z = 0; };

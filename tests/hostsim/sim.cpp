@@ -7,6 +7,9 @@
 #include "../../pde-engine_amd/csrc/pdeval_point.h"
 using namespace pd;
 
+static double g_om2 = 0.0;   // force-free Omega^2 (pdeval_params.omega2)
+extern "C" void sim_set_omega2(double w) { g_om2 = w; }
+
 extern "C" int sim_point(int problem, const int32_t* w, int nw, double x, double y, int tier2,
                          double* jet, double* err, double* res) {
     constexpr int MAXD = PDEVAL_MAX_STACK;
@@ -21,10 +24,10 @@ extern "C" int sim_point(int problem, const int32_t* w, int nw, double x, double
                        : I::run(w, 1, nw, x, y, u, stk.data(), 0, P);
         if (rc) return rc;
         for (int i = 0; i < 15; ++i) { jet[i] = u.c[i]; err[i] = e[i]; }
-        PointResult r = ff_epilogue<double>(u.c, x);
+        PointResult r = ff_epilogue<double>(u.c, x, g_om2);
         res[0] = r.res_abs;
         res[1] = r.scale;
-        res[2] = tier2 ? residual_noise<PDEVAL_PROBLEM_FORCE_FREE, double>(u.c, e, x, nullptr, r.scale) : 0.0;
+        res[2] = tier2 ? residual_noise<PDEVAL_PROBLEM_FORCE_FREE, double>(u.c, e, x, nullptr, r.scale, g_om2) : 0.0;
         res[3] = r.finite;
         return 0;
     }

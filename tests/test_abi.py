@@ -41,11 +41,12 @@ def test_opcodes_match_header():
 
 def test_params_struct_layout():
     import ctypes as C
-    assert C.sizeof(_lib.Params) == 64
+    assert C.sizeof(_lib.Params) == 72
     assert C.sizeof(_lib.Outputs) == 64
     p = _lib.default_params(0)
     assert p.tau_point == 1e-10 and p.kerr_abs_tol == 1e-10 and p.full_grid == 1
     assert p.point_abs_tol == 1e-20 and p.res_rel_acc == 1e-11 and p.noise_kappa == 16.0
+    assert p.omega2 == 0.0
     assert int(re.search(r'PDEVAL_N_PASSES\s+(\d+)', HEADER).group(1)) == _lib.N_PASSES
     assert int(re.search(r'PDEVAL_IMM_DD\s+\(1u << (\d+)\)', HEADER).group(1)) == OPC.IMM_DD.bit_length() - 1
 
@@ -75,3 +76,16 @@ def test_create_without_gpu_fails_loudly():
         pytest.skip('GPU present')
     with pytest.raises(_lib.PdevalError):
         _lib.Context(0)
+
+
+def test_plugin_omega_contract():
+    """Omega != 0 (validator.py:326-329): a constant whose square is an exact double is taken
+    (params.omega2 on the device); a symbolic Omega -- the reference allows a function of u --
+    or an inexact square raises NotImplementedError before any GPU use."""
+    from pdeval.batch import omega2_value
+    from problems.force_free.validator import PreciseFoliationValidator
+    assert omega2_value(1) == 1.0 and omega2_value('1/2') == 0.25 and omega2_value('sqrt(2)') == 2.0
+    assert PreciseFoliationValidator(Omega=1)._omega_key == '1'
+    for bad in ('1/3', 0.3, 'rho'):
+        with pytest.raises(NotImplementedError):
+            PreciseFoliationValidator(Omega=bad)

@@ -492,3 +492,32 @@ def test_plugin_api_depth5_sample():
         assert x is not None and (x['ok'], x['reason']) == (r['ok'], r['reason']), (r['expr'], r['reason'])
     assert {r['expr'] for r in bad} >= G.FF_D5_SYMBOLIC_DIVERGENCE
     assert len(bad) <= 0.02 * len(rows), [r['expr'] for r in bad]
+
+
+def test_plugin_omega1_reference_verdicts():
+    """Rotating field lines on the GPU: PreciseFoliationValidator(Omega=1) -- params.omega2 = 1,
+    the rotation terms of the device's epilogue in every tier -- gives the reference's verdict
+    and text on every decided row it ran with Omega = 1 (the 7 known solutions and a seeded
+    d <= 3 sample, tests/golden/ref/ff_omega1_*.jsonl), through trees and through strings."""
+    from problems import load_problem
+    from problems.force_free.validator import PreciseFoliationValidator
+    import sympy as sp
+    rows = G.decided(G.ref_rows('ff_omega1_known.jsonl', 'ff_omega1_d3_s600.jsonl'))
+    prob = load_problem('force_free')
+    locs = {**prob.symbols, **prob.constants, **prob.unary_ops}
+    v = PreciseFoliationValidator(Omega=1)
+    got = v.validate_batch([sp.sympify(r['expr'], locals=locs) for r in rows], check_regularity=False,
+                           fast_point_only=False)
+    bad = [(r['expr'], r['reason'], g) for g, r in zip(got, rows) if g != (r['ok'], r['reason'])]
+    # (only the symbolic stage's branch text of a grid reject: reproduced in 'text' mode below)
+    assert all(g[0] is False and 'expanded det' in rr for _, rr, g in bad) and len(bad) <= 2, bad[:5]
+    if bad:
+        vt = PreciseFoliationValidator(Omega=1, symbolic='text')
+        assert vt.validate_batch([sp.sympify(e, locals=locs) for e, _, _ in bad], check_regularity=False) == \
+            [(False, rr) for _, rr, _ in bad]
+    got_s = v.validate_strings([r['expr'] for r in rows])
+    assert got_s == got
+    # and Omega = 0 is untouched: the default validator's verdicts on the same rows differ
+    # exactly where the reference's do (Dipolar, Bent ... pass at Omega = 0)
+    v0 = PreciseFoliationValidator()
+    assert v0.validate(sp.sympify('rho**2*exp(-2*z)'), check_regularity=False)[0] is True

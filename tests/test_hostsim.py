@@ -30,6 +30,7 @@ def sim():
     lib = C.CDLL(SO)
     vp = C.c_void_p
     lib.sim_point.argtypes = [C.c_int, vp, C.c_int, C.c_double, C.c_double, C.c_int, vp, vp, vp]
+    lib.sim_set_omega2.argtypes = [C.c_double]
     lib.sim_point_tier.argtypes = [C.c_int, vp, C.c_int, C.c_int, C.c_int, vp]
     return lib
 
@@ -40,8 +41,22 @@ EXPRS = ['rho**2 + z**2', 'z*neg(rho/z + 1)', 'exp(z/(-rho**2 + z**2))',
          'log(rho + z**2)*z', 'rho/Abs(z)', '1/(1 - 1/(-rho**2 + z**2 + 1))', 'z**4/(rho**3 + 2)']
 
 
+@pytest.mark.parametrize('omega2', [0.0, 1.0, 0.25])
 @pytest.mark.parametrize('s', EXPRS)
-def test_device_source_matches_oracle(sim, s):
+def test_device_source_matches_oracle(sim, s, omega2):
+    """The device epilogue (jets; with Omega != 0 the rotation corrections ff_rotate_A / _B)
+    against the oracle's closed-form partials, at Omega = 0 (the problem path) and for rotating
+    field lines (validator.py:326-329)."""
+    sim.sim_set_omega2(omega2)
+    O.set_omega2(omega2)
+    try:
+        _device_source_matches_oracle(sim, s)
+    finally:
+        sim.sim_set_omega2(0.0)
+        O.set_omega2(0.0)
+
+
+def _device_source_matches_oracle(sim, s):
     pd_ = P.force_free()
     w = np.array(pd_.compile(pd_.parse(s)), dtype=np.int32)
     for pt in ((1.3, -0.55), (2.2, 1.1), (0.8, 6 / 7), (0.37, 1.9)):

@@ -294,6 +294,11 @@ def _hostpool_faults_body():
             time.sleep(0.1)
         assert not hostpool.active()
         assert hostpool.run(_square, list(range(10)), min_items=1) == [i * i for i in range(10)]
+        # (the collector thread terminates the surviving children after marking the pool
+        # broken; under load that takes a moment)
+        t0 = time.time()
+        while any(p.is_alive() for p in hostpool._POOL.procs) and time.time() - t0 < 20:
+            time.sleep(0.1)
         assert all(not p.is_alive() for p in hostpool._POOL.procs)
         assert pids
     finally:

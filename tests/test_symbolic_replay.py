@@ -41,6 +41,8 @@ def _ref_symbolic_rows():
         if not name.startswith('ff_') or not name.endswith('.jsonl'):
             continue
         for r in G.decided(G.ref_rows(name)):
+            if r.get('omega', '0') != '0':      # (rotating-field rows: test_oracle_omega1_*)
+                continue
             rs = r['reason']
             if r['ok'] or 'Lean could not' in rs or 'expanded det' in rs or 'simplify det' in rs:
                 out.setdefault(r['expr'], r)
