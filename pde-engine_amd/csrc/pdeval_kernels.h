@@ -552,6 +552,9 @@ struct PointResult {
 // behind a uniform branch, so the Omega = 0 epilogue is the same code as before.
 // MAG = true evaluates the same expression on magnitudes with every difference turned into
 // a sum: S >= sum of |monomials| of the fully expanded determinant.
+#ifndef PD_BSYM
+#define PD_BSYM 0
+#endif
 template <class T, bool MAG> struct FFEpi {
     // Everything is read straight from u's Taylor coefficients (no materialized copies of
     // p = u_rho, q = u_z), and each intermediate dies as soon as its Lie derivative is
@@ -608,6 +611,23 @@ template <class T, bool MAG> struct FFEpi {
         {
             // B = p^2 + q^2   (validator.py:324), order 2
             T B[6];
+#if PD_BSYM
+            // the square of a jet: each cross product once, doubled (2 p_a p_b, a != b) --
+            // 22 multiply-adds instead of 30
+            {
+                const T p00 = P(u, 0, 0), p10 = P(u, 1, 0), p01 = P(u, 0, 1);
+                const T p20 = P(u, 2, 0), p11 = P(u, 1, 1), p02 = P(u, 0, 2);
+                const T q00 = Q(u, 0, 0), q10 = Q(u, 1, 0), q01 = Q(u, 0, 1);
+                const T q20 = Q(u, 2, 0), q11 = Q(u, 1, 1), q02 = Q(u, 0, 2);
+                const T p00d = p00 + p00, q00d = q00 + q00, p10d = p10 + p10, q10d = q10 + q10;
+                B[ji(0, 0)] = fmac(p00, p00, q00 * q00);
+                B[ji(1, 0)] = fmac(p00d, p10, q00d * q10);
+                B[ji(0, 1)] = fmac(p00d, p01, q00d * q01);
+                B[ji(2, 0)] = fmac(p10, p10, fmac(q10, q10, fmac(p00d, p20, q00d * q20)));
+                B[ji(1, 1)] = fmac(p10d, p01, fmac(q10d, q01, fmac(p00d, p11, q00d * q11)));
+                B[ji(0, 2)] = fmac(p01, p01, fmac(q01, q01, fmac(p00d, p02, q00d * q02)));
+            }
+#else
 #pragma unroll
             for (int d = 0; d <= 2; ++d)
 #pragma unroll
@@ -625,6 +645,7 @@ template <class T, bool MAG> struct FFEpi {
                         }
                     B[ji(i, j)] = s;
                 }
+#endif
             if (om2 != 0.0) rotate_B(B, rho, om2);
             lie1(u, B, LB);
         }
