@@ -553,7 +553,7 @@ struct PointResult {
 // MAG = true evaluates the same expression on magnitudes with every difference turned into
 // a sum: S >= sum of |monomials| of the fully expanded determinant.
 #ifndef PD_BSYM
-#define PD_BSYM 0
+#define PD_BSYM 1
 #endif
 template <class T, bool MAG> struct FFEpi {
     // Everything is read straight from u's Taylor coefficients (no materialized copies of
