@@ -555,6 +555,9 @@ struct PointResult {
 #ifndef PD_BSYM
 #define PD_BSYM 1
 #endif
+#ifndef PD_AFMA
+#define PD_AFMA 1
+#endif
 template <class T, bool MAG> struct FFEpi {
     // Everything is read straight from u's Taylor coefficients (no materialized copies of
     // p = u_rho, q = u_z), and each intermediate dies as soon as its Lie derivative is
@@ -598,12 +601,18 @@ template <class T, bool MAG> struct FFEpi {
 #pragma unroll
                 for (int j = 0; j <= d; ++j) {
                     const int i = d - j;
-                    T s = U(u, i + 2, j) * (double)((i + 1) * (i + 2));
-                    s = fmac(U(u, i, j + 2), from_real<T>((double)((j + 1) * (j + 2))), s);
                     T pr = P(u, i, j) * ri[0];
 #pragma unroll
                     for (int i1 = 1; i1 <= i; ++i1) pr = fmac(P(u, i - i1, j), cvt<T>(ri[i1]), pr);
+#if PD_AFMA
+                    // u_rr + u_zz accumulated onto -p/rho: two FMAs, no separate add
+                    T s = fmac(U(u, i, j + 2), from_real<T>((double)((j + 1) * (j + 2))), sgn(pr));
+                    A[ji(i, j)] = fmac(U(u, i + 2, j), from_real<T>((double)((i + 1) * (i + 2))), s);
+#else
+                    T s = U(u, i + 2, j) * (double)((i + 1) * (i + 2));
+                    s = fmac(U(u, i, j + 2), from_real<T>((double)((j + 1) * (j + 2))), s);
                     A[ji(i, j)] = s + sgn(pr);
+#endif
                 }
             if (om2 != 0.0) rotate_A(A, u, rho, om2);
             lie1(u, A, LA);
