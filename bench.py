@@ -460,16 +460,19 @@ def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):
     return out
 
 
-def worker_pool(ref_batches, n_items, batch, procs):
+def worker_pool(ref_batches, n_items, batch, procs, passes=3):
     """N worker processes on one GPU (scripts/worker_child.py), the reference's --validators N
     (general_method_paper_reproduction.py:802-823): each takes every N-th queue batch of the
     same stream and runs process_batches; started as child processes (no exec in this one),
-    timed from a common start line to the last result.  Their result tuples are compared with
+    timed from a common start line to the last result.  Each process goes over its share
+    ``passes`` times (a worker drains a continuous queue: its pipeline fills once, which on one
+    142,004-row pass is a tenth of the time).  Their result tuples are compared with
     process_batch's, batch by batch (SHA-256 of each process's tuples in its own order)."""
     import hashlib
     import subprocess
     script = os.path.join(ROOT, 'scripts', 'worker_child.py')
-    ps = [subprocess.Popen([sys.executable, script, '--part', str(k), '--parts', str(procs), '--batch', str(batch)],
+    ps = [subprocess.Popen([sys.executable, script, '--part', str(k), '--parts', str(procs), '--batch', str(batch),
+                            '--passes', str(passes)],
                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True) for k in range(procs)]
     try:
         for p in ps:
@@ -493,12 +496,12 @@ def worker_pool(ref_batches, n_items, batch, procs):
     same = True
     for k, r in enumerate(res):
         h = hashlib.sha256()
-        for rb in ref_batches[k::procs]:
+        for rb in ref_batches[k::procs] * passes:
             h.update(repr(rb).encode())
         same = same and h.hexdigest() == r['digest']
     rows = sum(r['rows'] for r in res)
-    return {'processes': procs, 'rows': rows, 'seconds': round(wall, 3),
-            'candidates_per_s': round(rows / wall) if rows == n_items else None,
+    return {'processes': procs, 'passes': passes, 'rows': rows, 'seconds': round(wall, 3),
+            'candidates_per_s': round(rows / wall) if rows == n_items * passes else None,
             'per_process_s': [round(r['seconds'], 3) for r in res], 'tuples_identical': same}
 
 

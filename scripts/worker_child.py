@@ -7,7 +7,7 @@ over them.
 
 Protocol: prints READY once its context, SymPy pool and tagger are warm; waits for one line
 on stdin; then prints one JSON line {rows, seconds, digest} where digest is the SHA-256 of the
-repr of its result tuples, batch by batch in its own order."""
+repr of its result tuples, batch by batch in its own order (over all --passes)."""
 import argparse
 import hashlib
 import json
@@ -24,6 +24,8 @@ def main():
     ap.add_argument('--part', type=int, required=True)
     ap.add_argument('--parts', type=int, required=True)
     ap.add_argument('--batch', type=int, default=4096)
+    ap.add_argument('--passes', type=int, default=1,
+                    help='run over its batches this many times (a continuous queue: the pipeline fill once)')
     a = ap.parse_args()
     from pdeval import hostpool
     hostpool.start(local_workers=a.parts)     # forked before this process touches the GPU
@@ -43,7 +45,7 @@ def main():
     h = hashlib.sha256()
     n = 0
     t0 = time.perf_counter()
-    for r in process_batches(iter(mine), prob.validator, kw, locs, tagger):
+    for r in process_batches(iter(mine * a.passes), prob.validator, kw, locs, tagger):
         n += len(r)
         h.update(repr(r).encode())
     dt = time.perf_counter() - t0
