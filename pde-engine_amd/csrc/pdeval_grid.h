@@ -332,6 +332,10 @@ template <int W> struct PowTab {
 #ifndef PD_EPI_TABLE_RCP
 #define PD_EPI_TABLE_RCP 1
 #endif
+// the row's 1/x^2 and 1/x^3 moved into SGPRs (uniform_f64) rather than left in VGPRs
+#ifndef PD_EPI_UNIFORM
+#define PD_EPI_UNIFORM 1
+#endif
 // the per-point scaled residual by reciprocal + Newton steps instead of an IEEE division
 // (scaled_fast)
 #ifndef PD_FAST_SCALED
@@ -796,11 +800,18 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     const int groups = (a.nx + W - 1) / W;
     const int row0 = W * (int)((int64_t)groups * part / parts), row1 = min(a.nx, W * (int)((int64_t)groups * (part + 1) / parts));
     for (int row = row0; row < row1; row += W) {
-        double x[W], inv_x[W];
+        double x[W], inv_x[W], inv_x2[W], inv_x3[W];
 #pragma unroll
         for (int q = 0; q < W; ++q) {
             x[q] = rd_sf64(a.gx + min(row + q, a.nx - 1));   // a tail row past nx: unused
             inv_x[q] = rd_sf64(a.gx + a.nx + min(row + q, a.nx - 1));   // = rcp(x[q]), host table
+            // the epilogue's 1/x^2, 1/x^3 (as ff_epilogue_r forms them), kept in SGPRs
+            inv_x2[q] = inv_x[q] * inv_x[q];
+            inv_x3[q] = inv_x2[q] * inv_x[q];
+            if constexpr (PD_EPI_UNIFORM) {
+                inv_x2[q] = uniform_f64(inv_x2[q]);
+                inv_x3[q] = uniform_f64(inv_x3[q]);
+            }
         }
         PowTab<W> pt;
         pt.sx = a.nx * (K + 1);
@@ -837,7 +848,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 const int base = a.n_ref + (row + q) * a.ny + sl * 64;   // point index of lane 0
                 PointResult r;
                 if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE)
-                    r = PD_EPI_TABLE_RCP ? ff_epilogue_r<T>(u[q].c, inv_x[q], x[q], ROT ? a.prm.omega2 : 0.0)
+                    r = PD_EPI_TABLE_RCP ? ff_epilogue_p<T>(u[q].c, inv_x[q], inv_x2[q], inv_x3[q], x[q], ROT ? a.prm.omega2 : 0.0)
                                          : ff_epilogue<T>(u[q].c, x[q], ROT ? a.prm.omega2 : 0.0);
                 else r = kerr_epilogue<T>(u[q].c, kv[q]);
                 const double qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);

@@ -192,6 +192,16 @@ __device__ __forceinline__ double rd_sf64(const double* p) {
     return *p;
 #endif
 }
+// a value the caller knows to be the same in every lane, moved into scalar registers (a row's
+// powers of 1/x: held in VGPRs they cost the interpreter 4 of its registers)
+__device__ __forceinline__ double uniform_f64(double v) {
+#ifndef PD_HOST_SIM
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(v)));
+#else
+    return v;
+#endif
+}
 // an immediate that may be one of the problem's constants (PDEVAL_IMM_PRM)
 __device__ __forceinline__ double rd_immp(const int32_t* p, uint32_t w, const PrmTab<double>& P) {
     if (w & PDEVAL_IMM_PRM) return prm_value(P, rd_word(p));
@@ -590,8 +600,13 @@ template <class T, bool MAG> struct FFEpi {
     template <class R> static PD_HD T eval(const T* u, R rho, double om2 = 0.0) { return eval_r(u, rcp(rho), rho, om2); }
     template <class R> static PD_HD T eval_r(const T* u, R r0) { return eval_r(u, r0, r0, 0.0); }
     template <class R> static PD_HD T eval_r(const T* u, R r0, R rho, double om2) {
+        const R r2 = r0 * r0;
+        return eval_p(u, r0, r2, r2 * r0, rho, om2);
+    }
+    // r2 = r0 * r0, r3 = r2 * r0 (the lean grid passes hand in their row's wave-uniform copies)
+    template <class R> static PD_HD T eval_p(const T* u, R r0, R r2, R r3, R rho, double om2) {
         // 1/rho jet in the rho direction: (-1)^i / rho^(i+1)
-        const R ri[3] = {r0, r0 * r0 * (MAG ? 1.0 : -1.0), r0 * r0 * r0};
+        const R ri[3] = {r0, r2 * (MAG ? 1.0 : -1.0), r3};
         T LA[3], LB[3];
         {
             // A = p_rho + q_z - p / rho   (validator.py:323), order 2
@@ -712,8 +727,8 @@ template <class T, bool MAG> struct FFEpi {
 
 // (inv_rho = rcp(rho): the lean grid passes read it from the grid's reciprocal table instead of
 // dividing once per row; ff_epilogue below divides)
-template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T* u, double inv_rho, double rho = 0.0,
-                                                                       double om2 = 0.0) {
+template <class T> __device__ __forceinline__ PointResult ff_epilogue_p(const T* u, double inv_rho, double r2, double r3,
+                                                                       double rho, double om2) {
     PointResult r;
 #ifdef PD_VAR_NO_EPI   // timing variant: no determinant at all (verdicts meaningless)
     {
@@ -726,7 +741,7 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T*
         return r;
     }
 #endif
-    const T det = FFEpi<T, false>::eval_r(u, inv_rho, rho, om2);
+    const T det = FFEpi<T, false>::eval_p(u, inv_rho, r2, r3, rho, om2);
     // keep the signed and the magnitude evaluations apart: interleaved, the scheduler keeps
     // both sets of intermediates live
     __builtin_amdgcn_sched_barrier(0);
@@ -738,9 +753,9 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T*
         double m[15];
 #pragma unroll
         for (int i = 0; i < 15; ++i) m[i] = mag(u[i]);
-        S = FFEpi<double, true>::eval_r(m, inv_rho, rho, om2);
+        S = FFEpi<double, true>::eval_p(m, inv_rho, r2, r3, rho, om2);
     } else {
-        S = FFEpi<double, true>::eval_r(u, inv_rho, rho, om2);
+        S = FFEpi<double, true>::eval_p(u, inv_rho, r2, r3, rho, om2);
     }
 #endif
     r.res_abs = mag(det);
@@ -758,6 +773,12 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T*
     for (int i = 0; i < 15; ++i) fin = fin && jet_coef_ok(u[i]);
     r.finite = fin;
     return r;
+}
+
+template <class T> __device__ __forceinline__ PointResult ff_epilogue_r(const T* u, double inv_rho, double rho = 0.0,
+                                                                       double om2 = 0.0) {
+    const double r2 = inv_rho * inv_rho;
+    return ff_epilogue_p<T>(u, inv_rho, r2, r2 * inv_rho, rho, om2);
 }
 
 template <class T> __device__ __forceinline__ PointResult ff_epilogue(const T* u, double rho, double om2 = 0.0) {
