@@ -299,7 +299,19 @@ static int build_points(pdeval_ctx* c) {
     for (int i = 0; i < nx; ++i) gx.push_back(1.0 / gx[i]);
     HIPCHK(c, hipMemcpy(c->d_gx, gx.data(), 2 * nx * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_gy, gy.data(), ny * sizeof(double), hipMemcpyHostToDevice));
-    if (kerr) HIPCHK(c, hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (kerr) {
+        // then the same table with k1, k2 doubled (2 k is exact): the lean grid passes' copy,
+        // whose epilogue then forms 2 k u_rr, 2 k u_xx without the two multiplies per point
+        const size_t n4 = kc.size();
+        kc.resize(2 * n4);
+        for (size_t p = 0; p < n4; p += 4) {
+            kc[n4 + p] = 2.0 * kc[p];
+            kc[n4 + p + 1] = 2.0 * kc[p + 1];
+            kc[n4 + p + 2] = kc[p + 2];
+            kc[n4 + p + 3] = kc[p + 3];
+        }
+        HIPCHK(c, hipMemcpy(c->d_kc, kc.data(), kc.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     // the lean passes' coordinate-power tables, from the grid just uploaded (same JetOps::pcoefs)
     if (!c->d_ptab) HIPCHK(c, hipMalloc(&c->d_ptab, ptab_bytes(c->problem, nx, ny)));
     launch_ptab(c->problem, c->d_gx, c->d_gy, nx, ny, c->d_ptab, c->stream);
@@ -404,7 +416,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if ((e = hipMalloc(&c->d_gx, 2 * nx * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
     if ((e = hipMalloc(&c->d_gy, ny * sizeof(double))) != hipSuccess) return fail("hipMalloc", e);
     if (problem_id == PDEVAL_PROBLEM_KERR &&
-        (e = hipMalloc(&c->d_kc, 4 * (size_t)c->n_pts * sizeof(double))) != hipSuccess)
+        (e = hipMalloc(&c->d_kc, 8 * (size_t)c->n_pts * sizeof(double))) != hipSuccess)
         return fail("hipMalloc", e);
     if (problem_id == PDEVAL_PROBLEM_KERR) pdeval_default_kerr_constants(&c->kconst);
     if (int rc = build_points(c)) {
@@ -690,6 +702,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.nx = c->nx;
     a.ny = c->ny;
     a.kc = c->d_kc;
+    a.kc2 = c->d_kc ? c->d_kc + 4 * (size_t)c->n_pts : nullptr;
     a.ptab = c->d_ptab;
     a.n_ref = c->n_ref;
     a.n_pts = c->n_pts;
@@ -1300,6 +1313,7 @@ extern "C" int pdeval_point_eval(pdeval_ctx* c, const int32_t* prog, int64_t n_w
     for (int k = 0; k < 16; ++k) a.kc_ref[k] = c->kc_ref[k];
     copy_constants(c, a);
     a.kc = c->d_kc;
+    a.kc2 = c->d_kc ? c->d_kc + 4 * (size_t)c->n_pts : nullptr;
     a.ptab = c->d_ptab;
     a.n_ref = c->n_ref;
     a.prm = prm;

@@ -332,9 +332,19 @@ template <int W> struct PowTab {
 #ifndef PD_EPI_TABLE_RCP
 #define PD_EPI_TABLE_RCP 1
 #endif
-// the row's 1/x^2 and 1/x^3 moved into SGPRs (uniform_f64) rather than left in VGPRs
+// the row's 1/x^2 and 1/x^3 moved into SGPRs (uniform_f64) rather than left in VGPRs: the pass-1
+// spill drops from 64 to 32 B, but the same-box A/B (r04_w) measured no gain, so it stays off
+// Kerr: the lean epilogue (kerr_epilogue_lean: the doubled coefficient table, one maximum for
+// the coefficient tests)
+#ifndef PD_KERR_LEAN
+#define PD_KERR_LEAN 1
+#endif
+// keep the lane's 1/y out of the row loop (pin_f64 above)
+#ifndef PD_INVY_PIN
+#define PD_INVY_PIN 1
+#endif
 #ifndef PD_EPI_UNIFORM
-#define PD_EPI_UNIFORM 1
+#define PD_EPI_UNIFORM 0
 #endif
 // the per-point scaled residual by reciprocal + Newton steps instead of an IEEE division
 // (scaled_fast)
@@ -784,7 +794,11 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     }
     const int per_row = a.ny >> 6;
     const double y0 = a.gy[lane];
-    const double inv_y0 = rcp(y0);
+    double inv_y0 = rcp(y0);
+    // opaque to the optimizer: otherwise "per_row == 1 ? inv_y0 : rcp(y)" below is rewritten as
+    // rcp(per_row == 1 ? y0 : y) and the IEEE reciprocal (11 VALU) runs once per row instead of
+    // once per candidate
+    if constexpr (PD_INVY_PIN) pin_f64(inv_y0);
     double qmax = 0.0;
     int nbad = 0, nfin = 0;
     bool grad_nz = (ps & P0_GRAD) != 0;
@@ -822,7 +836,8 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
         for (int sl = 0; sl < per_row; ++sl) {
             const double y = per_row == 1 ? y0 : a.gy[sl * 64 + lane];
             pt.py = a.ptab + (size_t)PTAB_N * a.nx * (K + 1) + sl * 64 + lane;
-            const double inv_y = per_row == 1 ? inv_y0 : rcp(y);
+            double inv_y = inv_y0;
+            if (per_row != 1) inv_y = rcp(y);
             // Kerr: this point's operator coefficients (a 128 KiB table, L2-resident) are loaded
             // before the program runs, so their latency hides under the interpreter
             // (W > 2: after it, so that 4W doubles are not live through the interpreter)
@@ -831,7 +846,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 if constexpr (PROB != PDEVAL_PROBLEM_FORCE_FREE) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        const double* kp = a.kc + 4 * (a.n_ref + min(row + q, a.nx - 1) * a.ny + sl * 64 + lane);
+                        const double* kp = (PD_KERR_LEAN ? a.kc2 : a.kc) + 4 * (a.n_ref + min(row + q, a.nx - 1) * a.ny + sl * 64 + lane);
 #pragma unroll
                         for (int i = 0; i < 4; ++i) kv[q][i] = kp[i];
                     }
@@ -850,6 +865,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE)
                     r = PD_EPI_TABLE_RCP ? ff_epilogue_p<T>(u[q].c, inv_x[q], inv_x2[q], inv_x3[q], x[q], ROT ? a.prm.omega2 : 0.0)
                                          : ff_epilogue<T>(u[q].c, x[q], ROT ? a.prm.omega2 : 0.0);
+                else if constexpr (PD_KERR_LEAN && !Real<T>::cplx_pass) r = kerr_epilogue_lean<T>(u[q].c, kv[q]);
                 else r = kerr_epilogue<T>(u[q].c, kv[q]);
                 const double qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
                 if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {

@@ -54,6 +54,7 @@ struct KernelArgs {
     const double* gy;           // ny grid ordinates (ny % 64 == 0)
     int nx, ny;
     const double* kc;           // Kerr: 4 operator coefficients per point (NULL for FF)
+    const double* kc2;          // Kerr: the same with the first two doubled (lean grid passes)
     // coordinate-power tables of the lean grid passes (pdeval_grid.h ptab_kernel, built once per
     // context), or NULL: the jets C(n,k) v^(n-k), k <= K, of v**n for 0 <= n <= 16 at every
     // grid abscissa ([n][row][k], wave-uniform) and ordinate ([n][k][j], lane j)
@@ -200,6 +201,15 @@ __device__ __forceinline__ double uniform_f64(double v) {
                             __builtin_amdgcn_readfirstlane(__double2loint(v)));
 #else
     return v;
+#endif
+}
+// a value the optimizer must treat as unknown from here on (no rematerialization, no
+// rewriting of expressions that use it)
+__device__ __forceinline__ void pin_f64(double& v) {
+#ifndef PD_HOST_SIM
+    asm volatile("" : "+v"(v));
+#else
+    (void)v;
 #endif
 }
 // an immediate that may be one of the problem's constants (PDEVAL_IMM_PRM)
@@ -817,6 +827,46 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue(const T*
         allz = allz && is_zero(u[i]);
     }
     r.finite = fin && !allz;
+    return r;
+}
+
+// max(|a|, |b|) in one v_max_f64 with both source modifiers.  The compiler's fmax first
+// canonicalizes each operand (one more v_max per operand) to quiet a signalling NaN; the one
+// caller below gives a NaN no meaning, so the bare instruction is enough.
+__device__ __forceinline__ double max_abs(double a, double b) {
+#ifndef PD_HOST_SIM
+    double r;
+    asm volatile("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+#else
+    return fmax(fabs(a), fabs(b));
+#endif
+}
+
+// kerr_epilogue for the lean grid passes (real jets): k2 = {2 k1, 2 k2, k3, k4} (the doubled
+// table, kc2), and the coefficient tests folded into one maximum -- the same PointResult,
+// bit for bit:
+//  * every t_i finite <=> S finite, and then |L| <= S (rounding is monotone), so L is finite;
+//  * m = max |c| over the five coefficients: all zero <=> m == 0, all below kHugeJet <=>
+//    m < kHugeJet, unless a coefficient is NaN (v_max drops a quiet NaN) -- a NaN in u_r, u_x,
+//    u_rr or u_xx makes S NaN, and u itself is tested on its own; with a NaN "finite" is false
+//    whatever m says.
+template <class T> __device__ __forceinline__ PointResult kerr_epilogue_lean(const T* u, const double* k2) {
+    static_assert(!Real<T>::cplx_pass, "real jets only");
+    PointResult r;
+    const double t1 = u[ji(2, 0)] * k2[0];
+    const double t2 = u[ji(0, 2)] * k2[1];
+    const double t3 = u[ji(1, 0)] * k2[2];
+    const double t4 = u[ji(0, 1)] * k2[3];
+    const double L = (t1 + t2) + (t3 + t4);
+    r.scale = (fabs(t1) + fabs(t2)) + (fabs(t3) + fabs(t4));
+    r.res_abs = fabs(L);
+    r.res_re = L;
+    r.res_im = 0.0;
+    r.grad_zero = u[ji(1, 0)] == 0.0 && u[ji(0, 1)] == 0.0;
+    const double m = max_abs(max_abs(max_abs(u[ji(0, 0)], u[ji(1, 0)]), max_abs(u[ji(0, 1)], u[ji(2, 0)])),
+                             u[ji(0, 2)]);
+    r.finite = isfinite(r.scale) && !isnan(u[ji(0, 0)]) && m < kHugeJet && m != 0.0;
     return r;
 }
 
