@@ -96,3 +96,19 @@ extern "C" int sim_point_tier(int problem, const int32_t* w, int nw, int k, int 
     if (tier == 2) return run_tier<PDEVAL_PROBLEM_KERR, dd, dd>(a, w, nw, k, out);
     return -1;
 }
+
+// kerr_epilogue (every tier) and kerr_epilogue_lean (the lean grid passes, doubled table) on
+// one jet u[6] and coefficients k[4]: out = {res_abs, scale, res_re, finite, grad_zero} of each
+extern "C" void sim_kerr_epi_pair(const double* u, const double* k, double* out) {
+    const double k2[4] = {2.0 * k[0], 2.0 * k[1], k[2], k[3]};
+    const PointResult a = kerr_epilogue<double>(u, k);
+    const PointResult b = kerr_epilogue_lean<double>(u, k2);
+    const PointResult* r[2] = {&a, &b};
+    for (int i = 0; i < 2; ++i) {
+        out[5 * i + 0] = r[i]->res_abs;
+        out[5 * i + 1] = r[i]->scale;
+        out[5 * i + 2] = r[i]->res_re;
+        out[5 * i + 3] = r[i]->finite ? 1.0 : 0.0;
+        out[5 * i + 4] = r[i]->grad_zero ? 1.0 : 0.0;
+    }
+}

@@ -74,3 +74,36 @@ def _device_source_matches_oracle(sim, s):
         # residuals agree to the noise bound, and the noise bounds to a factor 4
         assert abs(res[0] - o[0]) <= 4 * max(o[2], res[2]) + 1e-12 * o[1], (s, pt, res, o)
         assert res[2] <= 4 * o[2] + 1e-300 and o[2] <= 4 * res[2] + 1e-300, (s, pt, res[2], o[2])
+
+
+def test_kerr_lean_epilogue_equals_kerr_epilogue(sim):
+    """The lean grid passes' Kerr epilogue (doubled coefficient table, one maximum for the
+    coefficient tests) gives the PointResult of kerr_epilogue bit for bit, on random jets and on
+    every special value in every coefficient (NaN, +-inf, the 2^160 bound, zeros, subnormals)."""
+    sim.sim_kerr_epi_pair.argtypes = [C.c_void_p] * 3
+    rng = np.random.default_rng(7)
+    specials = [np.nan, np.inf, -np.inf, 0.0, -0.0, 2.0 ** 160, -(2.0 ** 160), np.nextafter(2.0 ** 160, 0),
+                5e-324, 1e308, -1e308, 1.0]
+    cases = []
+    for _ in range(2000):
+        u = rng.standard_normal(6) * 10.0 ** rng.integers(-30, 30, 6)
+        k = rng.standard_normal(4) * 10.0 ** rng.integers(-5, 5, 4)
+        cases.append((u, k))
+    for i in range(6):
+        for v in specials:
+            for base in (np.zeros(6), np.ones(6), rng.standard_normal(6)):
+                u = base.copy()
+                u[i] = v
+                cases.append((u, rng.standard_normal(4)))
+                cases.append((u, np.array([0.0, 1.0, 0.0, 1.0])))
+    cases.append((np.zeros(6), np.zeros(4)))
+    cases.append((np.array([0, 0, 0, 1e300, 0, 1e300]), np.array([1e10, 1e10, 1.0, 1.0])))
+    out = np.zeros(10)
+    bad = []
+    for u, k in cases:
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        k = np.ascontiguousarray(k, dtype=np.float64)
+        sim.sim_kerr_epi_pair(u.ctypes.data, k.ctypes.data, out.ctypes.data)
+        if out[:5].tobytes() != out[5:].tobytes():
+            bad.append((u.tolist(), k.tolist(), out.tolist()))
+    assert not bad, bad[:3]
