@@ -627,8 +627,11 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
 // Tier B: the point stage in double-double (T = dd, or cdd for complex candidates), final,
 // one candidate per lane over a device list.  MAXD = 2: operand stack in LDS (the common
 // case); deeper or complex programs: private memory.
+// waves/SIMD of the stack-2 double-double kernel: at 1 its register spill goes to AGPRs
+// (scratch 0, 144 B/lane at 2), and the same-box A/B (profiles/r04_z*) measured no difference in
+// the 2^21 step or the worker batch's device call
 #ifndef PD_DD2_WAVES
-#define PD_DD2_WAVES 2
+#define PD_DD2_WAVES 1
 #endif
 // the double-double class s of a candidate, applied to its final grid class
 __device__ __forceinline__ void dd_apply_one(const KernelArgs& a, int64_t cand, uint8_t s) {
