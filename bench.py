@@ -34,7 +34,8 @@ sys.path.insert(0, os.path.join(ROOT, 'tests'))
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector peak (spec; MI355X_MICROARCH.md lists FP32 157.3 = 2x)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s"
-DOMINANT = 'grid_kernel<0, false>'   # pass 1 (force-free, full-batch instance); Kerr: grid_kernel<1, false>
+# pass 1 (force-free, full-batch instance, Omega = 0); Kerr: grid_kernel<1, false, false>
+DOMINANT = 'grid_kernel<0, false, false>'
 
 
 def load_workload(problem):
@@ -57,7 +58,9 @@ def pmc_traffic(n_per_launch, dominant=DOMINANT):
     for path in reversed(files):          # the newest summary (by name) that has the kernel
         with open(path) as f:
             s = json.load(f)
-        k = s.get('kernels', {}).get(dominant)
+        kern = s.get('kernels', {})
+        # summaries from before the ROT instances name the kernel without its third argument
+        k = kern.get(dominant) or kern.get(dominant.replace(', false, false>', ', false>'))
         if k and k.get('candidates') and 'hbm_bytes_per_launch' in k:
             return k['hbm_bytes_per_launch'] / k['candidates'] * n_per_launch, os.path.basename(path)
     return None, None
@@ -121,7 +124,7 @@ def main():
     pid = PROBLEM_FORCE_FREE if a.problem == 'force_free' else PROBLEM_KERR
 
     slug = 'force_free' if pid == PROBLEM_FORCE_FREE else 'kerr_magnetosphere'
-    dominant = f'grid_kernel<{pid}, false>'
+    dominant = f'grid_kernel<{pid}, false, false>'
     wname, ops_all, off_all, exprs_all = load_workload(slug)
     nprog = len(off_all) - 1
     total = a.n * world
