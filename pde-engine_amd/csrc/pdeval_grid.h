@@ -339,6 +339,10 @@ template <int W> struct PowTab {
 #ifndef PD_KERR_LEAN
 #define PD_KERR_LEAN 1
 #endif
+// the per-point scaled residual as a select, no branch (scaled_sel)
+#ifndef PD_SCALED_SEL
+#define PD_SCALED_SEL 0
+#endif
 // keep the lane's 1/y out of the row loop (pin_f64 above)
 #ifndef PD_INVY_PIN
 #define PD_INVY_PIN 1
@@ -867,7 +871,8 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                                          : ff_epilogue<T>(u[q].c, x[q], ROT ? a.prm.omega2 : 0.0);
                 else if constexpr (PD_KERR_LEAN && !Real<T>::cplx_pass) r = kerr_epilogue_lean<T>(u[q].c, kv[q]);
                 else r = kerr_epilogue<T>(u[q].c, kv[q]);
-                const double qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
+                const double qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale)
+                                  : PD_SCALED_SEL ? scaled_sel(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
                 if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {

@@ -875,6 +875,14 @@ __device__ __forceinline__ double scaled(double res_abs, double S) {
     return res_abs == 0.0 ? 0.0 : INFINITY;
 }
 
+// scaled() as a select: the division runs in every lane (a lane with S <= 0 or NaN discards
+// it), so the per-point test has no divergent branch and no exec-mask bookkeeping; same value
+__device__ __forceinline__ double scaled_sel(double res_abs, double S) {
+    const double q = res_abs / S;
+    const double alt = res_abs == 0.0 ? 0.0 : INFINITY;
+    return S > 0.0 ? q : alt;
+}
+
 // scaled() for the lean grid passes' per-point test: res_abs * 1/S with the hardware
 // reciprocal and two Newton steps (5 VALU against the 10 of the IEEE division sequence, which
 // the Kerr epilogue pays per point beside ~20 others).  Relative error ~2^-52 -- far below the
