@@ -341,7 +341,7 @@ template <int W> struct PowTab {
 #endif
 // the per-point scaled residual as a select, no branch (scaled_sel)
 #ifndef PD_SCALED_SEL
-#define PD_SCALED_SEL 0
+#define PD_SCALED_SEL 1
 #endif
 // keep the lane's 1/y out of the row loop (pin_f64 above)
 #ifndef PD_INVY_PIN
