@@ -38,6 +38,15 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s"
 DOMINANT = 'grid_kernel<0, false, false>'
 
 
+_T0 = time.perf_counter()
+
+
+def log(msg):
+    """A progress line on stderr (the JSON result is the only stdout line): every leg reports,
+    so no stretch of the run is silent for minutes."""
+    print(f'[bench {time.perf_counter() - _T0:7.1f}s] {msg}', file=sys.stderr, flush=True)
+
+
 def load_workload(problem):
     # force-free: the depth-4 validated set; Kerr (SURVEY.md §8d C5): the whole depth<=4 stream
     # (1,024,799 candidates; the pre-validate filters keep 1,999 of a 2,000 seeded sample, so
@@ -110,9 +119,8 @@ def main():
     import torch
     import torch.distributed as dist
     from pdeval import _lib
-    from pdeval.opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR, FP_N, FLAG_COMPLEX
-    from pdeval.shard import gather_verdicts, gather_verdicts_native, init_native_comm
-    from pdeval import workload as WL
+    from pdeval.opcodes import PROBLEM_FORCE_FREE, PROBLEM_KERR
+    from pdeval.shard import gather_verdicts, gather_verdicts_native, init_native_comm, pack_bits
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -123,124 +131,71 @@ def main():
     dev = torch.device(f'cuda:{local}')
     pid = PROBLEM_FORCE_FREE if a.problem == 'force_free' else PROBLEM_KERR
 
-    slug = 'force_free' if pid == PROBLEM_FORCE_FREE else 'kerr_magnetosphere'
-    dominant = f'grid_kernel<{pid}, false, false>'
-    wname, ops_all, off_all, exprs_all = load_workload(slug)
-    nprog = len(off_all) - 1
+    log(f'loading {a.problem} workload, {a.n} candidates per GPU')
+    pb = ProblemBench(pid, a.n, world, rank, local, dev)
+    log('workload resident in HBM')
+    slug, ctx, idx, n, ranges = pb.slug, pb.ctx, pb.idx, pb.n, pb.ranges
+    ops, off, ops_all, off_all, exprs_all, nprog = pb.ops, pb.off, pb.ops_all, pb.off_all, pb.exprs_all, pb.nprog
     total = a.n * world
-    # (experiment PD_BENCH_STREAM_ORDER: keep the stream order)
-    tiled = WL.tiled_indices(nprog, total, seed=0, shuffle=not os.environ.get('PD_BENCH_STREAM_ORDER'))
-    # algorithmic work of the batch; it also balances the shards
-    flops_prog = WL.flops_per_program(pid, ops_all, off_all)
-    plan = WL.rank_plan(tiled, world, rank, flops_prog)
-    ranges, idx, n = plan.ranges, plan.idx, plan.n
-    ops, off = WL.gather_programs(ops_all, off_all, idx)
-    ctx = _lib.Context(pid, device=local)
-    npts, nref = ctx.n_points, ctx.n_ref
-    flops_step = float(flops_prog[idx].sum()) * npts
-    out_bytes_per = 1 + 8 + 8 * nref + 8 + 4 + 4 + 8 * FP_N + 1.0 / 8
-    bytes_step = ops.nbytes + off.nbytes + n * out_bytes_per
-
-    d_ops = torch.from_numpy(ops).to(dev)
-    d_off = torch.from_numpy(off).to(dev)
-    outs = dict(verdict_bits=torch.zeros(((n + 31) // 32) * 4, dtype=torch.uint8, device=dev),
-                status=torch.zeros(n, dtype=torch.uint8, device=dev),
-                q_ref=torch.zeros(n, dtype=torch.float64, device=dev),
-                res_ref=torch.zeros(n * nref, dtype=torch.float64, device=dev),
-                q_grid=torch.zeros(n, dtype=torch.float64, device=dev),
-                n_bad=torch.zeros(n, dtype=torch.int32, device=dev),
-                n_nonfinite=torch.zeros(n, dtype=torch.int32, device=dev),
-                fingerprint=torch.zeros(n * FP_N, dtype=torch.float64, device=dev))
-    d_out = _lib.Outputs(*[outs[f].data_ptr() for f, _ in _lib.Outputs._fields_])
     prm = _lib.default_params(pid)
     prm.full_grid = 0 if a.early_exit else 1
-    # all uploads / zero-fills above ran on torch's default stream: finish them, then run the
-    # hot path on a dedicated stream that the events below are recorded on
-    torch.cuda.synchronize(dev)
-    stream = torch.cuda.Stream(dev)
 
-    def step(p):
-        ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out,
-                            params=p, stream=stream.cuda_stream, zero_bits=True)
+    elapsed, kern_ms = pb.timed(prm, a.steps, a.warmup)
+    log(f'timed: {a.steps} steps, {elapsed / a.steps * 1e3:.2f} ms per step')
 
-    def timed(p, steps, warmup):
-        for _ in range(warmup):
-            step(p)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(steps)]
+    # After the timed region: the final (plugin) verdicts of this rank's shard -- the device
+    # outputs through the host steps (pdeval.shard.final_verdicts, once per distinct program of
+    # the tiled batch) -- then the one exchange step, an all-gather of the re-packed bitmaps over
+    # RCCL through the C ABI (pdeval_gather_bits), checked against torch.distributed's.
+    dev_out = pb.host_outputs()
+    status_dev = dev_out['status'].copy()
+    if world > 1 or not a.no_extras:
         t0 = time.perf_counter()
-        for s, e in ev:
-            s.record(stream)
-            step(p)
-            e.record(stream)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        el = time.perf_counter() - t0
-        kern = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()), kern
-
-    elapsed, kern_ms = timed(prm, a.steps, a.warmup)
-
-    # the one exchange step: all-gather of the verdict bitmaps over RCCL, through the C ABI
-    # (pdeval_gather_bits), checked against torch.distributed's all-gather
-    gather = None
+        final = pb.final_verdicts(dev_out, prm)
+        t_host = time.perf_counter() - t0
+        log(f'final verdicts (host steps) {t_host:.2f} s')
+        gather = {'bits': 'final (device + host steps)', 'host_steps_s': round(t_host, 3),
+                  'host_step_changes_local': int((dev_out['status'] != status_dev).sum())}
+    else:   # (--no-extras at one GPU: timing runs, the device bitmap as it stands)
+        final = status_dev == 0
+        gather = {'bits': 'device (--no-extras)'}
     if world > 1:
-        verdict_all = gather_verdicts(outs['verdict_bits'], ranges)
+        bits = torch.from_numpy(pack_bits(final)).to(dev)
+        verdict_all = gather_verdicts(bits, ranges)
         try:
             init_native_comm(ctx, rank, world)
             t0 = time.perf_counter()
-            native = gather_verdicts_native(ctx, outs['verdict_bits'], ranges)
-            gather = {'native_rccl_ms': round((time.perf_counter() - t0) * 1e3, 3),
-                      'native_equals_torch': bool(np.array_equal(native, verdict_all))}
+            native = gather_verdicts_native(ctx, bits, ranges)
+            gather.update(native_rccl_ms=round((time.perf_counter() - t0) * 1e3, 3),
+                          native_equals_torch=bool(np.array_equal(native, verdict_all)))
             verdict_all = native
         except Exception as e:   # noqa: BLE001 -- reported; the torch gather result stands
-            gather = {'native_rccl_error': str(e)[:200]}
+            gather['native_rccl_error'] = str(e)[:200]
     else:
-        verdict_all = np.unpackbits(outs['verdict_bits'].cpu().numpy(), bitorder='little')[:n].astype(bool)
-    status = outs['status'].cpu().numpy()
+        verdict_all = final
+    status = dev_out['status']
+    if not a.no_extras and rank == 0:
+        # the single-process plugin's verdicts on the same global batch: every distinct program
+        # once through pdeval_validate_batch + the host steps, mapped onto the tiled batch
+        plugin = pb.plugin_verdicts(prm)[pb.tiled]
+        log('plugin verdicts')
+        gather['final_equals_plugin'] = bool(np.array_equal(verdict_all, plugin))
+        gather['device_bits_equal_plugin'] = None if world > 1 else bool(
+            np.array_equal(np.unpackbits(pb.outs['verdict_bits'].cpu().numpy(), bitorder='little')[:n].astype(bool),
+                           plugin))
 
     # size-independent checks at full size: duplicates of one program (the batch is tiled)
     # get one class, and the streamable paper solutions are accepted wherever they occur
     first = np.full(nprog, 255, dtype=np.int16)
-    first[idx[::-1]] = status[::-1]
-    consistent = bool(np.array_equal(first[idx], status))
+    first[idx[::-1]] = status_dev[::-1]
+    consistent = bool(np.array_equal(first[idx], status_dev))
 
-    # per-pass device times (library HIP events on the launch stream) for the dominant
-    # kernel's roofline: pass 1 = programs of stack <= 2 in real arithmetic
-    ctx.set_timing(True)
-    pass_ms = {}
-    for _ in range(a.steps):
-        step(prm)
-        for k, v in ctx.pass_times().items():
-            pass_ms[k] = pass_ms.get(k, 0.0) + v / a.steps
-    counts = ctx.pass_counts()
-    ctx.set_timing(False)
-    hdr = ops[off[:-1]].astype(np.int64)
-    depth = (hdr >> 8) & 0xff
-    cflag = (hdr & FLAG_COMPLEX) != 0
-    in_p1 = (depth <= 2) & ~cflag
-    fl = flops_prog[idx]
-    # candidates pass 1 re-routed to the complex pass after the point stage: their grid work
-    # is not pass 1's (charged at the pass-1 mean, a conservative correction)
-    rerouted = max(0, counts['complex'] - int(cflag.sum())) if pid == PROBLEM_FORCE_FREE else 0
-    p1_flops = (float(fl[in_p1].sum()) - rerouted * float(fl[in_p1].mean() if in_p1.any() else 0.0)) * npts
-    p1_ms = pass_ms['pass1_stack2']
+    prof = pb.profile(prm, a.steps)
+    log('per-pass profile')
 
     res = None
     if rank == 0:
         value = total * a.steps / elapsed
-        achieved_tf = p1_flops / (p1_ms * 1e-3) / 1e12
-        achieved_gbs = bytes_step / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(int(in_p1.sum()), dominant)
         res = {
             'metric': ('validated candidates/sec (force-free depth-4 batch, 64x64 grid + p*)'
                        if pid == PROBLEM_FORCE_FREE else
@@ -248,37 +203,38 @@ def main():
             'value': value, 'unit': 'candidates/s', 'n_gpus': world, 'steps': a.steps,
             'warmup': a.warmup, 'ms_per_step': elapsed / a.steps * 1e3, 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic',
-            'config': {'workload': f'{slug} validated candidates ({wname}, {nprog} '
+            'config': {'workload': f'{slug} validated candidates ({pb.wname}, {nprog} '
                                    f'programs) tiled+shuffled(seed 0) to {a.n}/GPU; 64x64 grid + ref point',
-                       'problem': a.problem, 'candidates_per_gpu': a.n, 'points_per_candidate': npts,
+                       'problem': a.problem, 'candidates_per_gpu': a.n, 'points_per_candidate': pb.npts,
                        'full_grid': not a.early_exit, 'parallelism': f'shard{world}'},
-            'roofline': {'bound': 'valu_fp64', 'kernel': dominant, 'achieved': achieved_tf,
-                         'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS,
-                         'traffic': traffic, 'traffic_source': traffic_src,
-                         'kernel_ms': p1_ms, 'kernel_candidates': int(in_p1.sum()) - rerouted,
-                         'flops_per_launch': p1_flops},
-            'roofline_hbm': {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS,
-                             'unit': 'GB/s', 'frac': achieved_gbs / HBM_PEAK_GBS,
-                             'bytes_per_step': bytes_step, 'step_ms': kern_ms},
-            'pass_ms': {k: round(v, 3) for k, v in pass_ms.items()},
-            'work_lists': counts,
+            'roofline': prof['roofline'],
+            'roofline_hbm': pb.roofline_hbm(kern_ms),
+            'pass_ms': prof['pass_ms'],
+            'work_lists': prof['counts'],
             'accepted': int(verdict_all.sum()),
+            'accepted_device_bits': int((status_dev == 0).sum()) if world == 1 else None,
             'status_hist': np.bincount(status, minlength=8).tolist(),
             'duplicates_consistent': consistent,
+            'gather': gather,
         }
-        if gather is not None:
-            res['gather'] = gather
         if world > 1:
             res['shard_balance'] = 'flops'
+        if not a.no_extras and world == 1 and pid == PROBLEM_FORCE_FREE:
+            # configs[4]'s operator on the same build, measured by the driver's own command:
+            # the Kerr depth<=4 stream at the same per-GPU batch (the weakest kernel, pass 1)
+            log('Kerr sub-record')
+            res['kerr'] = kerr_subrecord(a.n, a.steps, a.warmup, world, rank, local, dev)
+            log('Kerr sub-record done')
 
     if not a.no_extras and world == 1:
+        log('early-exit / host-buffer / time-to-solutions legs')
         # the reference's control flow: stop after the point stage for point-rejects (same
         # verdicts; reported beside, never as, the headline value)
         pe = _lib.default_params(pid)
         pe.full_grid = 0
-        bits_full = outs['verdict_bits'].clone()
-        el_e, _ = timed(pe, a.steps, 1)
-        same = bool(torch.equal(bits_full, outs['verdict_bits']))
+        bits_full = pb.outs['verdict_bits'].clone()
+        el_e, _ = pb.timed(pe, a.steps, 1)
+        same = bool(torch.equal(bits_full, pb.outs['verdict_bits']))
         res['value_early_exit'] = total * a.steps / el_e
         res['early_exit_verdicts_identical'] = same
         # host buffers in and out (PCIe-inclusive), one synchronous C-ABI call
@@ -316,20 +272,228 @@ def main():
                 'hybrid_compile_s': round(t_comp, 4)}
 
     if not a.no_extras and world == 1 and pid == PROBLEM_FORCE_FREE:
+        log('strict-mode leg')
+        res['strict'] = strict_leg(exprs_all, local)
+        res['value_strict'] = res['strict']['value_strict']
         # the worker pool's batch path, queue tuples in -> result tuples out (the reference's
         # _parallel_validator_worker protocol, general_method_paper_reproduction.py:1756-1816)
+        log('worker / inline legs')
         res['worker_process_batch'] = worker_throughput(exprs_all)
 
     if rank == 0:
         if not a.no_cpu and world == 1:
             procs = a.cpu_procs or int(os.environ.get('OMP_NUM_THREADS', '0') or os.cpu_count())
             if pid == PROBLEM_FORCE_FREE:
+                log(f'SymPy CPU baseline ({a.sympy_seconds:.0f} s budget, {procs} processes)')
                 res['cpu_baseline'] = cpu_baseline_sympy(procs, a.sympy_seconds)
+            log('C-oracle CPU baseline')
             res['cpu_baseline_c_port'] = cpu_baseline(pid, ops_all, off_all, idx, a.cpu_seconds)
         print(json.dumps(res))
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+class ProblemBench:
+    """One problem's workload on this rank's GPU: the tiled batch's shard resident in HBM, the
+    library context, the output buffers and the launch stream the events are recorded on."""
+
+    def __init__(self, pid, n_per_rank, world, rank, local, dev):
+        import torch
+        from pdeval import _lib
+        from pdeval.opcodes import PROBLEM_FORCE_FREE, FP_N
+        from pdeval import workload as WL
+        self.pid, self.world, self.rank, self.dev = pid, world, rank, dev
+        self.slug = 'force_free' if pid == PROBLEM_FORCE_FREE else 'kerr_magnetosphere'
+        self.dominant = f'grid_kernel<{pid}, false, false>'
+        self.wname, self.ops_all, self.off_all, self.exprs_all = load_workload(self.slug)
+        self.nprog = len(self.off_all) - 1
+        # (experiment PD_BENCH_STREAM_ORDER: keep the stream order)
+        self.tiled = WL.tiled_indices(self.nprog, n_per_rank * world, seed=0,
+                                      shuffle=not os.environ.get('PD_BENCH_STREAM_ORDER'))
+        # algorithmic work of the batch (DESIGN.md §7); it also balances the shards
+        self.flops_prog = WL.flops_per_program(pid, self.ops_all, self.off_all)
+        plan = WL.rank_plan(self.tiled, world, rank, self.flops_prog)
+        self.ranges, self.idx, self.n = plan.ranges, plan.idx, plan.n
+        self.ops, self.off = WL.gather_programs(self.ops_all, self.off_all, self.idx)
+        self.ctx = _lib.Context(pid, device=local)
+        self.npts, self.nref = self.ctx.n_points, self.ctx.n_ref
+        out_bytes_per = 1 + 8 + 8 * self.nref + 8 + 4 + 4 + 8 * FP_N + 1.0 / 8
+        self.bytes_step = self.ops.nbytes + self.off.nbytes + self.n * out_bytes_per
+        n = self.n
+        self.d_ops = torch.from_numpy(self.ops).to(dev)
+        self.d_off = torch.from_numpy(self.off).to(dev)
+        self.outs = dict(verdict_bits=torch.zeros(((n + 31) // 32) * 4, dtype=torch.uint8, device=dev),
+                         status=torch.zeros(n, dtype=torch.uint8, device=dev),
+                         q_ref=torch.zeros(n, dtype=torch.float64, device=dev),
+                         res_ref=torch.zeros(n * self.nref, dtype=torch.float64, device=dev),
+                         q_grid=torch.zeros(n, dtype=torch.float64, device=dev),
+                         n_bad=torch.zeros(n, dtype=torch.int32, device=dev),
+                         n_nonfinite=torch.zeros(n, dtype=torch.int32, device=dev),
+                         fingerprint=torch.zeros(n * FP_N, dtype=torch.float64, device=dev))
+        self.d_out = _lib.Outputs(*[self.outs[f].data_ptr() for f, _ in _lib.Outputs._fields_])
+        # all uploads / zero-fills above ran on torch's default stream: finish them, then run the
+        # hot path on a dedicated stream that the events below are recorded on
+        torch.cuda.synchronize(dev)
+        self.stream = torch.cuda.Stream(dev)
+
+    def step(self, p):
+        self.ctx.validate_device(self.d_ops.data_ptr(), self.d_ops.numel(), self.d_off.data_ptr(), self.n,
+                                 self.d_out, params=p, stream=self.stream.cuda_stream, zero_bits=True)
+
+    def timed(self, p, steps, warmup):
+        """(max over ranks of the wall time of `steps` steps, mean event time of one step)"""
+        import torch
+        import torch.distributed as dist
+        dev = self.dev
+        for _ in range(warmup):
+            self.step(p)
+        torch.cuda.synchronize(dev)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        t0 = time.perf_counter()
+        for s, e in ev:
+            s.record(self.stream)
+            self.step(p)
+            e.record(self.stream)
+        torch.cuda.synchronize(dev)
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        kern = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), kern
+
+    def host_outputs(self) -> dict:
+        """The device outputs of the last step as host arrays (res_ref, fingerprint 2-D)."""
+        r = {k: v.cpu().numpy() for k, v in self.outs.items() if k != 'verdict_bits'}
+        r['res_ref'] = r['res_ref'].reshape(self.n, self.nref)
+        r['fingerprint'] = r['fingerprint'].reshape(self.n, -1)
+        r['verdict'] = r['status'] == 0
+        return r
+
+    def _kerr(self):
+        from pdeval.opcodes import PROBLEM_KERR
+        from pdeval._lib import default_kerr_constants
+        return default_kerr_constants() if self.pid == PROBLEM_KERR else None
+
+    def final_verdicts(self, r, prm):
+        """This rank's final verdicts: its device outputs through the host steps, once per
+        distinct program of the shard (pdeval.shard.final_verdicts)."""
+        from pdeval import problem_defs as P
+        from pdeval.shard import final_verdicts
+        items = _LazyItems(self.exprs_all, self.idx)
+        return final_verdicts(P.get(self.slug), self._kerr(), prm, self.npts - self.nref, items, r,
+                              self.ops, self.off, keys=self.idx)
+
+    def plugin_verdicts(self, prm) -> np.ndarray:
+        """The single-process plugin's verdict of every program of the table: one
+        pdeval_validate_batch from host buffers + the host steps (BatchValidator's path)."""
+        from pdeval import problem_defs as P
+        from pdeval.batch import apply_host_steps
+        r = self.ctx.validate(self.ops_all, self.off_all, prm)
+        apply_host_steps(P.get(self.slug), self._kerr(), prm, self.npts - self.nref,
+                         _LazyItems(self.exprs_all, None), r, self.ops_all, self.off_all)
+        return np.asarray(r['verdict'], dtype=bool)
+
+    def profile(self, prm, steps) -> dict:
+        """Per-pass device times (library HIP events on the launch stream) and the dominant
+        kernel's roofline: pass 1 = programs of stack <= 2 in real arithmetic."""
+        from pdeval.opcodes import PROBLEM_FORCE_FREE, FLAG_COMPLEX
+        ctx = self.ctx
+        ctx.set_timing(True)
+        pass_ms = {}
+        for _ in range(steps):
+            self.step(prm)
+            for k, v in ctx.pass_times().items():
+                pass_ms[k] = pass_ms.get(k, 0.0) + v / steps
+        counts = ctx.pass_counts()
+        ctx.set_timing(False)
+        hdr = self.ops[self.off[:-1]].astype(np.int64)
+        depth = (hdr >> 8) & 0xff
+        cflag = (hdr & FLAG_COMPLEX) != 0
+        in_p1 = (depth <= 2) & ~cflag
+        fl = self.flops_prog[self.idx]
+        # candidates pass 1 re-routed to the complex pass after the point stage: their grid work
+        # is not pass 1's (charged at the pass-1 mean, a conservative correction)
+        rerouted = max(0, counts['complex'] - int(cflag.sum())) if self.pid == PROBLEM_FORCE_FREE else 0
+        p1_flops = (float(fl[in_p1].sum()) - rerouted * float(fl[in_p1].mean() if in_p1.any() else 0.0)) * self.npts
+        p1_ms = pass_ms['pass1_stack2']
+        achieved_tf = p1_flops / (p1_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic(int(in_p1.sum()), self.dominant)
+        roof = {'bound': 'valu_fp64', 'kernel': self.dominant, 'achieved': achieved_tf,
+                'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS,
+                'traffic': traffic, 'traffic_source': traffic_src,
+                'kernel_ms': p1_ms, 'kernel_candidates': int(in_p1.sum()) - rerouted,
+                'flops_per_launch': p1_flops}
+        roof.update(pmc_flop_frac(self.dominant, int(in_p1.sum()) - rerouted, p1_ms))
+        return {'roofline': roof, 'pass_ms': {k: round(v, 3) for k, v in pass_ms.items()}, 'counts': counts}
+
+    def roofline_hbm(self, kern_ms) -> dict:
+        achieved_gbs = self.bytes_step / (kern_ms * 1e-3) / 1e9
+        return {'bound': 'hbm', 'achieved': achieved_gbs, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                'frac': achieved_gbs / HBM_PEAK_GBS, 'bytes_per_step': self.bytes_step, 'step_ms': kern_ms}
+
+    def close(self):
+        self.ctx.close()
+
+
+class _LazyItems:
+    """exprs[idx[i]] as a read-only sequence of str (the tiled batch's candidate strings,
+    without a 2^21-element list)."""
+
+    def __init__(self, exprs, idx):
+        self.exprs, self.idx = exprs, idx
+
+    def __len__(self):
+        return len(self.exprs) if self.idx is None else len(self.idx)
+
+    def __getitem__(self, i):
+        return str(self.exprs[i if self.idx is None else self.idx[i]])
+
+
+def kerr_subrecord(n, steps, warmup, world, rank, local, dev):
+    """configs[4]'s operator (Kerr depth <= 4 stream, 2^21 candidates per GPU) on the same build,
+    in the default bench run: value, per-pass times and the pass-1 roofline."""
+    from pdeval import _lib
+    from pdeval.opcodes import PROBLEM_KERR
+    kb = ProblemBench(PROBLEM_KERR, n, world, rank, local, dev)
+    try:
+        prm = _lib.default_params(PROBLEM_KERR)
+        el, kern_ms = kb.timed(prm, steps, warmup)
+        prof = kb.profile(prm, steps)
+        return {'metric': 'validated candidates/sec (Kerr depth<=4 batch, 64x64 grid + 3 reference points)',
+                'value': kb.n * world * steps / el, 'unit': 'candidates/s', 'ms_per_step': el / steps * 1e3,
+                'workload': f'{kb.wname} ({kb.nprog} programs) tiled+shuffled(seed 0) to {n}/GPU',
+                'roofline': prof['roofline'], 'pass_ms': prof['pass_ms'], 'work_lists': prof['counts']}
+    finally:
+        kb.close()
+
+
+def pmc_flop_frac(dominant, n_cand, kernel_ms):
+    """The dominant kernel's FP64 FLOP rate from the hardware counters (the newest committed
+    PMC summary with SQ FP64 counts: (2 FMA + MUL + ADD) x 64 lanes per wave = per candidate,
+    scaled to this launch's candidates and its event time), beside the FLOP model's fraction;
+    {} when no summary has them.  (TRANS -- rcp, sqrt estimates -- is not counted as FLOPs.)"""
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))
+    for path in reversed(files):
+        with open(path) as f:
+            s = json.load(f)
+        k = s.get('kernels', {}).get(dominant) or s.get('kernels', {}).get(dominant.replace(', false, false>', ', false>'))
+        if k and k.get('candidates') and 'SQ_INSTS_VALU_FMA_F64' in k:
+            fl = 64.0 * (2 * k['SQ_INSTS_VALU_FMA_F64'] + k.get('SQ_INSTS_VALU_MUL_F64', 0.0) +
+                         k.get('SQ_INSTS_VALU_ADD_F64', 0.0))
+            per = fl / k['candidates']
+            tf = per * n_cand / (kernel_ms * 1e-3) / 1e12
+            return {'counter_flops_per_candidate': per, 'counter_achieved': tf,
+                    'counter_frac': tf / FP64_PEAK_TFLOPS, 'counter_source': os.path.basename(path)}
+    return {}
 
 
 def _free_port():
@@ -386,6 +550,34 @@ def plan_record(a):
             'workload': wname, 'total': int(plan.total), 'range': [int(s0), int(s1)], 'n': plan.n,
             'flops': float(flops_prog[plan.idx].sum()), 'flops_total': float(flops_prog[tiled].sum()),
             'idx_head': [int(i) for i in plan.idx[:4]]}
+
+
+def strict_leg(exprs, device, n=1000, seed=0):
+    """The 'strict' symbolic mode (pdeval.symbolic.suspect + the reference's symbolic stage
+    replayed for the grid zeros of those shapes, 60 s per candidate over the SymPy pool) on a
+    seed-0 sample of the depth-4 strings: candidates/s end to end (compile, device, host steps),
+    the suspect fraction, and the default mode's rate on the same sample beside it.  A bounded
+    sample: the replays cost seconds each (the reference's own symbolic stage)."""
+    import random
+    from pdeval.batch import get_validator
+    sample = random.Random(seed).sample([str(e) for e in exprs], min(n, len(exprs)))
+    bv = get_validator('force_free', device)
+    out = {'sample': len(sample), 'timeout_s': bv.symbolic_timeout}
+    for mode in ('off', 'strict'):
+        t0 = time.perf_counter()
+        p = bv.prepare_strings(sample)
+        r = bv.run_prepared(p)
+        t = bv.finish(p, r, symbolic=mode)
+        dt = time.perf_counter() - t0
+        out[mode] = {'seconds': round(dt, 3), 'candidates_per_s': round(len(sample) / dt, 1),
+                     'accepted': int(np.asarray(t['ok']).sum())}
+        if mode == 'strict':
+            out[mode].update(t.get('strict', {}))
+    st = out['strict']
+    out['value_strict'] = out['strict']['candidates_per_s']
+    out['suspect_fraction'] = round(st.get('suspect', 0) / max(1, len(sample)), 4)
+    out['suspect_fraction_of_grid_zeros'] = round(st.get('suspect', 0) / max(1, st.get('grid_zero', 0)), 4)
+    return out
 
 
 def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):

@@ -306,6 +306,10 @@ static pt_result eval_point(int problem, const int32_t* w, int64_t nw, double x,
 }
 
 static double scaled(double a, double s) { return s > 0 ? a / s : (a == 0 ? 0 : INFINITY); }
+/* the grid's zero test, as the device applies it (pdeval_kernels.h grid_fails): a finite point
+ * fails iff |res| > tau S -- no division (equal to scaled(res, S) > tau except within a rounding
+ * of tau) */
+static int grid_fails(double a, double s, double tau) { return a > tau * s; }
 
 /* ---------------------------------------------------------------- point stage (quad)
  * The reference points as exact ratios, evaluated in __float128 (constants carry their
@@ -480,7 +484,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                 double q = scaled(r.res_abs, r.scale);
                 ++nfin;
                 if (q > qmax) qmax = q;
-                if (q > prm->tau_grid) ++nb;
+                if (grid_fails(r.res_abs, r.scale, prm->tau_grid)) ++nb;
                 if (!r.grad_zero) any_grad = 1;
             } else {
                 ++nnf;
@@ -494,7 +498,7 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                 int rc2;
                 pt_result r2 = eval_point(problem, w, nw, px[p], py[p], cplx, 1, &rc2, 1);
                 if (rc2 || !r2.finite) continue;
-                if (scaled(r2.res_abs, r2.scale) > prm->tau_grid && r2.res_abs > prm->noise_kappa * r2.noise) ++nb;
+                if (grid_fails(r2.res_abs, r2.scale, prm->tau_grid) && r2.res_abs > prm->noise_kappa * r2.noise) ++nb;
             }
         }
         if (cls < 0) {

@@ -116,6 +116,7 @@ struct pdeval_ctx {
     // buffer they reference is reallocated (buf_epoch)
     bool use_graph = true;          // env PDEVAL_GRAPH=0 turns it off
     uint64_t buf_epoch = 0;
+    void* h_errw = nullptr;        // pinned word: the device error word after a direct-path call
     struct GraphEntry {
         hipGraphExec_t exec = nullptr;
         uint64_t epoch = 0;
@@ -317,6 +318,9 @@ static int build_points(pdeval_ctx* c) {
     launch_ptab(c->problem, c->d_gx, c->d_gy, nx, ny, c->d_ptab, c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    // captured small-batch graphs hold the old constants by value (kc_ref, prm_pt / prm_grid,
+    // ct_x / ct_y in their kernel arguments): drop them, as after a buffer reallocation
+    ++c->buf_epoch;
     return PDEVAL_OK;
 }
 
@@ -424,7 +428,8 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
         pdeval_destroy(c);
         return rc;
     }
-    if ((e = hipMalloc(&c->d_counts, PD_N_LISTS * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
+    // the list counters and, after them, the device error word (KernelArgs::errw)
+    if ((e = hipMalloc(&c->d_counts, (PD_N_LISTS + 1) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
     *out = c;
     return PDEVAL_OK;
 }
@@ -452,6 +457,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     for (auto& g : c->graphs)
         if (g.second.exec) (void)hipGraphExecDestroy(g.second.exec);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->h_errw) (void)hipHostFree(c->h_errw);
     for (hipEvent_t& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
@@ -674,6 +680,12 @@ template <class T, int K, int MAXD> constexpr size_t tier2_lds() {
 #define PD_DD_EARLY_MIN_N 1024
 #endif
 
+// zeroes `words` 32-bit words (the list counters, a small batch's verdict bits) -- a kernel node
+// in the captured graphs rather than a memset node
+__global__ void zero_words_kernel(uint32_t* p, int64_t words) {
+    for (int64_t i = threadIdx.x; i < words; i += blockDim.x) p[i] = 0u;
+}
+
 template <int PROB>
 static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, const int64_t* d_off, int64_t n,
                       const pdeval_params& prm, const pdeval_outputs& o, hipStream_t s,
@@ -713,7 +725,12 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     if (!a.out.status) a.out.status = c->d_status;
     a.list_capacity = c->cap;
     int32_t* const cnt = c->d_counts;
-    HIPCHK(c, hipMemsetAsync(cnt, 0, PD_N_LISTS * sizeof(int32_t), s));
+    // (a kernel, not hipMemsetAsync: captured into the small-batch graphs, a memset node was
+    // seen to leave these counters unzeroed on replay -- the stale counts of an earlier, larger
+    // batch then sent the list passes to entries outside the batch, profiles/r05_e_pytest_gpu.log)
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, s, (uint32_t*)cnt, (int64_t)(PD_N_LISTS + 1));
+    HIPCHK(c, hipGetLastError());
+    a.errw = (uint32_t*)(cnt + PD_N_LISTS);
     constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
     constexpr bool FF = PROB == PDEVAL_PROBLEM_FORCE_FREE;
     constexpr int WPB = 4;  // waves (candidates) per 256-thread block of pass 1
@@ -979,6 +996,25 @@ extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64
 static constexpr int64_t kSmallWords = 4096;   // input capacity of the graph path (words)
 static constexpr int kGraphFallback = -1000;
 
+// the device error word of the last launch chain (KernelArgs::errw): a work-list entry outside
+// [0, n) was met and skipped -- the outputs of the call are not to be trusted
+static int check_errw(pdeval_ctx* c, uint32_t w, const char* path = "direct", int64_t n = -1, int captured = -1) {
+    if (!w) return PDEVAL_OK;
+    // the state of the call, for the report: list counters, capacity, the buffer epoch
+    int32_t h[PD_N_LISTS] = {0};
+    (void)hipMemcpy(h, c->d_counts, sizeof(h), hipMemcpyDeviceToHost);
+    std::string cnt;
+    for (int k = 0; k < PD_N_LISTS; ++k) cnt += (k ? "," : "") + std::to_string(h[k]);
+    char buf[256];
+    std::snprintf(buf, sizeof(buf),
+                  "device work-list check failed (kernel families 0x%x): a list entry outside the batch [%s n=%lld "
+                  "captured=%d cap=%lld epoch=%llu graphs=%zu counts=",
+                  (unsigned)w, path, (long long)n, captured, (long long)c->cap, (unsigned long long)c->buf_epoch,
+                  c->graphs.size());
+    c->err = std::string(buf) + cnt + "]";
+    return PDEVAL_ERR_HIP;
+}
+
 static int64_t outbuf_layout(const pdeval_ctx* c, int64_t n, pdeval_outputs* d) {
     const int64_t nb = ((n + 31) / 32) * 4;
     const int64_t sz_bits = (nb + 15) / 16 * 16, sz_st = (n + 15) / 16 * 16;
@@ -1030,8 +1066,8 @@ static int validate_small(pdeval_ctx* c, const int32_t* ops, int64_t n_words, co
     if (rc) return rc;
     const size_t in_bytes = kSmallWords * 4 + (PD_GRAPH_MAX_N + 1) * 8;
     if (!c->h_stage) {
-        HIPCHK(c, hipHostMalloc((void**)&c->h_stage, in_bytes + need_max, hipHostMallocDefault));
-        c->h_stage_bytes = in_bytes + need_max;
+        HIPCHK(c, hipHostMalloc((void**)&c->h_stage, in_bytes + need_max + 16, hipHostMallocDefault));
+        c->h_stage_bytes = in_bytes + need_max + 16;
     }
     pdeval_params prm;
     if (params) prm = *params;
@@ -1055,7 +1091,9 @@ static int validate_small(pdeval_ctx* c, const int32_t* ops, int64_t n_words, co
         c->graphs.erase(it);
         it = c->graphs.end();
     }
+    int fresh = 0;
     if (it == c->graphs.end()) {
+        fresh = 1;
         if (c->graphs.size() >= 256) {   // bounded cache
             for (auto& g : c->graphs) (void)hipGraphExecDestroy(g.second.exec);
             c->graphs.clear();
@@ -1063,7 +1101,8 @@ static int validate_small(pdeval_ctx* c, const int32_t* ops, int64_t n_words, co
         hipGraph_t g = nullptr;
         if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) return kGraphFallback;
         int lrc = PDEVAL_OK;
-        if (hipMemsetAsync(d.verdict_bits, 0, ((n + 31) / 32) * 4, s) != hipSuccess) lrc = PDEVAL_ERR_HIP;
+        hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, s, (uint32_t*)d.verdict_bits, (int64_t)((n + 31) / 32));
+        if (hipGetLastError() != hipSuccess) lrc = PDEVAL_ERR_HIP;
         if (lrc == PDEVAL_OK)
             lrc = c->problem == PDEVAL_PROBLEM_FORCE_FREE
                       ? launch_all<PDEVAL_PROBLEM_FORCE_FREE>(c, c->d_ops, c->hcap_words, c->d_off, n, prm, d, s, dmax)
@@ -1088,7 +1127,10 @@ static int validate_small(pdeval_ctx* c, const int32_t* ops, int64_t n_words, co
                              hipMemcpyHostToDevice, s));
     HIPCHK(c, hipGraphLaunch(it->second.exec, s));
     HIPCHK(c, hipMemcpyAsync(hout, c->d_outbuf, need, hipMemcpyDeviceToHost, s));
+    uint32_t* herr = reinterpret_cast<uint32_t*>(c->h_stage + in_bytes + need_max);
+    HIPCHK(c, hipMemcpyAsync(herr, c->d_counts + PD_N_LISTS, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    if (int erc = check_errw(c, *herr, "graph", n, fresh)) return erc;
     auto take = [&](void* h, const void* dv, size_t bytes) {
         if (h) std::memcpy(h, hout + ((const uint8_t*)dv - c->d_outbuf), bytes);
     };
@@ -1193,8 +1235,14 @@ extern "C" int pdeval_validate_batch(pdeval_ctx* c, const int32_t* ops, int64_t 
     if ((rc = dl(out->fingerprint, d.fingerprint, 8 * n * PDEVAL_FP_N))) return rc;
     if ((rc = dl(out->n_bad, d.n_bad, 4 * n))) return rc;
     if ((rc = dl(out->n_nonfinite, d.n_nonfinite, 4 * n))) return rc;
+    uint32_t* herr = reinterpret_cast<uint32_t*>(c->h_errw);
+    if (!herr) {
+        HIPCHK(c, hipHostMalloc((void**)&c->h_errw, 16, hipHostMallocDefault));
+        herr = reinterpret_cast<uint32_t*>(c->h_errw);
+    }
+    HIPCHK(c, hipMemcpyAsync(herr, c->d_counts + PD_N_LISTS, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    return PDEVAL_OK;
+    return check_errw(c, *herr, "direct", n);
 }
 
 extern "C" int pdeval_set_timing(pdeval_ctx* c, int enable) {

@@ -343,6 +343,11 @@ template <int W> struct PowTab {
 #ifndef PD_SCALED_SEL
 #define PD_SCALED_SEL 1
 #endif
+// the division-free zero test (grid_fails: |res| > tau S) and the lane's maximum of q as a
+// (|res|, S) pair divided once (GridMax), instead of q = |res| / S at every point
+#ifndef PD_DIVFREE
+#define PD_DIVFREE 1
+#endif
 // keep the lane's 1/y out of the row loop (pin_f64 above)
 #ifndef PD_INVY_PIN
 #define PD_INVY_PIN 1
@@ -360,7 +365,6 @@ template <class T, int K, int W, int MAXD> struct Lean {
     using J = typename O::J;
     static constexpr int NCJ = nc(K);
 
-    static constexpr int SLOT = W * NCJ * 64;   // T values per operand slot
     // Kerr (K = 2): the mixed coefficient u_rx feeds only itself through every jet operation
     // and the operator has no mixed term (kerr_epilogue), so it is not stored, not loaded and
     // forced to 0 after each opcode; the compiler then drops its arithmetic (PD_KERR_NOMIX=0:
@@ -368,6 +372,11 @@ template <class T, int K, int W, int MAXD> struct Lean {
     static constexpr bool NOMIX = PD_KERR_NOMIX && K == 2;
     static constexpr int MIX = ji(1, 1);
     static __device__ __forceinline__ bool live(int c) { return !(NOMIX && c == MIX); }
+    // LDS layout: the live coefficients only (Kerr: 5 of 6 -- an operand slot of W = 8 jets is
+    // 20 KiB per wave instead of 24, which is what 8 waves per CU fit in 160 KiB)
+    static constexpr int NCL = NCJ - (NOMIX ? 1 : 0);
+    static __device__ __forceinline__ constexpr int lidx(int c) { return NOMIX && c > MIX ? c - 1 : c; }
+    static constexpr int SLOT = W * NCL * 64;   // T values per operand slot
     static constexpr bool RSLOT = PD_LEAN_RSLOT && MAXD == 3;   // operand slot 1 in registers (run below)
     static constexpr int LDS_SLOTS = RSLOT ? 1 : MAXD - 1;
 
@@ -377,13 +386,13 @@ template <class T, int K, int W, int MAXD> struct Lean {
         for (int w = 0; w < W; ++w)
 #pragma unroll
             for (int c = 0; c < NCJ; ++c)
-                if (live(c)) stk[(w * NCJ + c) * 64 + lane] = t[w].c[c];
+                if (live(c)) stk[(w * NCL + lidx(c)) * 64 + lane] = t[w].c[c];
     }
     static __device__ __forceinline__ void load(const T* stk, int lane, J (&t)[W]) {
 #pragma unroll
         for (int w = 0; w < W; ++w)
 #pragma unroll
-            for (int c = 0; c < NCJ; ++c) t[w].c[c] = live(c) ? stk[(w * NCJ + c) * 64 + lane] : zero<T>();
+            for (int c = 0; c < NCJ; ++c) t[w].c[c] = live(c) ? stk[(w * NCL + lidx(c)) * 64 + lane] : zero<T>();
     }
 
     // Evaluate a decoded program (decode_kernel; `dec` at the program's header word) at
@@ -585,7 +594,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                         l = reg[RSLOT ? q : 0];
                     } else {
 #pragma unroll
-                        for (int c = 0; c < NCJ; ++c) l.c[c] = live(c) ? src[(q * NCJ + c) * 64 + lane] : zero<T>();
+                        for (int c = 0; c < NCJ; ++c) l.c[c] = live(c) ? src[(q * NCL + lidx(c)) * 64 + lane] : zero<T>();
                     }
                     if (op == PDOP_DIV) O::div(l, acc[q]);
                     else if (op == PDOP_SUB) O::sub(l, acc[q]);
@@ -746,8 +755,8 @@ template <int PROB, int MAXD> constexpr int grid_w() {
 template <int PROB> constexpr int grid_k() { return PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2; }
 // dynamic LDS of one block of `waves` waves: the LDS operand slots (Lean::LDS_SLOTS) of W jets
 template <int PROB, int MAXD, class T = double> constexpr size_t grid_lds(int waves) {
-    return (size_t)waves * Lean<T, grid_k<PROB>(), grid_w<PROB, MAXD>(), MAXD>::LDS_SLOTS * grid_w<PROB, MAXD>() *
-           nc(grid_k<PROB>()) * 64 * sizeof(T);
+    using L = Lean<T, grid_k<PROB>(), grid_w<PROB, MAXD>(), MAXD>;
+    return (size_t)waves * L::LDS_SLOTS * L::SLOT * sizeof(T);
 }
 
 // The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots, jets
@@ -803,6 +812,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     // rcp(per_row == 1 ? y0 : y) and the IEEE reciprocal (11 VALU) runs once per row instead of
     // once per candidate
     if constexpr (PD_INVY_PIN) pin_f64(inv_y0);
+    GridMax<PROB != PDEVAL_PROBLEM_FORCE_FREE> gm;   // (PD_DIVFREE) the lane's running maximum of q
     double qmax = 0.0;
     int nbad = 0, nfin = 0;
     bool grad_nz = (ps & P0_GRAD) != 0;
@@ -871,8 +881,13 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                                          : ff_epilogue<T>(u[q].c, x[q], ROT ? a.prm.omega2 : 0.0);
                 else if constexpr (PD_KERR_LEAN && !Real<T>::cplx_pass) r = kerr_epilogue_lean<T>(u[q].c, kv[q]);
                 else r = kerr_epilogue<T>(u[q].c, kv[q]);
-                const double qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale)
-                                  : PD_SCALED_SEL ? scaled_sel(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
+                // the zero test: |res| > tau S (PD_DIVFREE, no division per point; the lane's
+                // maximum of q is kept as a (|res|, S) pair and divided once, GridMax) or the
+                // round-4 form q = |res| / S per point, q > tau
+                double qv = 0.0;
+                if constexpr (!PD_DIVFREE)
+                    qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale)
+                                        : PD_SCALED_SEL ? scaled_sel(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
                 if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {
@@ -884,15 +899,23 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                         }
                     }
                 }
-                if (r.finite) {
-                    qmax = fmax(qmax, qv);
-                    if (!r.grad_zero) grad_nz = true;
+                if constexpr (PD_DIVFREE) {
+                    gm.add(r.finite, r.res_abs, r.scale);
+                    grad_nz = grad_nz | (r.finite & !r.grad_zero);
+                    nfin += count_lanes(r.finite);
+                    nbad += count_lanes(r.finite & grid_fails(r.res_abs, r.scale, a.prm.tau_grid));
+                } else {
+                    if (r.finite) {
+                        qmax = fmax(qmax, qv);
+                        if (!r.grad_zero) grad_nz = true;
+                    }
+                    nfin += (int)__popcll(__ballot(r.finite));
+                    nbad += (int)__popcll(__ballot(r.finite && qv > a.prm.tau_grid));
                 }
-                nfin += (int)__popcll(__ballot(r.finite));
-                nbad += (int)__popcll(__ballot(r.finite && qv > a.prm.tau_grid));
             }
         }
     }
+    if constexpr (PD_DIVFREE) qmax = gm.q();
     qmax = wave_max(qmax);
     bool grad_any = __any(grad_nz);
     if (parts > 1) {
@@ -972,7 +995,8 @@ void grid_kernel(KernelArgs a, int64_t* slow_list, int32_t* slow_count, int part
         wi /= parts;
     }
     if (wi >= a.n) return;
-    const int64_t cand = (PD_GRID_PERM && a.perm) ? (int64_t)__builtin_amdgcn_readfirstlane(a.perm[wi]) : wi;
+    const int64_t cand = (PD_GRID_PERM && a.perm) ? checked_cand(a, (int64_t)__builtin_amdgcn_readfirstlane(a.perm[wi]), ERRW_PERM) : wi;
+    if (cand < 0) return;
     grid_body<PROB, 2, double, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, part, parts);
 }
 
@@ -990,7 +1014,8 @@ __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST
     if (nwork > a.list_capacity) nwork = a.list_capacity;
     for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
         const int64_t wi = wp / parts;
-        const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
+        const int64_t cand = checked_cand(a, (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]), ERRW_GRID_LIST);
+        if (cand < 0) continue;
         grid_body<PROB, 3, double, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, (int)(wp % parts), parts);
     }
 }
@@ -1015,7 +1040,8 @@ __global__ __launch_bounds__(64, PD_CPLX_WAVES_PER_SIMD) void grid_cplx_kernel(K
     if (nwork > a.list_capacity) nwork = a.list_capacity;
     for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
         const int64_t wi = wp / parts;
-        const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
+        const int64_t cand = checked_cand(a, (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]), ERRW_CPLX);
+        if (cand < 0) continue;
         grid_body<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count,
                                                       (int)(wp % parts), parts);
     }

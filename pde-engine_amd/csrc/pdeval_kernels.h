@@ -87,7 +87,24 @@ struct KernelArgs {
     // Kerr constant test (pdeval_point.h): points where u's gradient must be rounding noise
     double ct_x[8], ct_y[8];
     int n_ct;
+    // device error word (d_counts[PD_N_LISTS], zeroed with the counters at every launch chain):
+    // bit k = a work-list entry outside [0, n) met by kernel family k (checked_cand), which is
+    // then skipped; the host turns a non-zero word into an error of the call
+    uint32_t* errw;
 };
+
+// A candidate index read from a work list or the shape permutation, checked: an entry outside
+// [0, n) -- a list read before its write completed, or a corrupt list -- is recorded in the
+// error word (bit `code`) and the caller skips it, instead of indexing the batch with it.
+enum : uint32_t {
+    ERRW_PERM = 1u, ERRW_GRID_LIST = 2u, ERRW_GENERIC = 4u, ERRW_POINT_LIST = 8u, ERRW_DD = 16u,
+    ERRW_DD_APPLY = 32u, ERRW_TIER2 = 64u, ERRW_CPLX = 128u
+};
+__device__ __forceinline__ int64_t checked_cand(const KernelArgs& a, int64_t cand, uint32_t code) {
+    if (cand >= 0 && cand < a.n) return cand;
+    if (a.errw) atomicOr(a.errw, code);
+    return -1;
+}
 
 // Partial grid counts of one tier-2 list entry whose grid is split over several waves.
 struct T2Acc {
@@ -778,9 +795,9 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_p(const T*
     }
     r.scale = S;
     r.grad_zero = is_zero(u[ji(1, 0)]) && is_zero(u[ji(0, 1)]);
-    bool fin = finite_(det) && isfinite(S);
+    bool fin = finite_(det) & isfinite(S);
 #pragma unroll
-    for (int i = 0; i < 15; ++i) fin = fin && jet_coef_ok(u[i]);
+    for (int i = 0; i < 15; ++i) fin = fin & jet_coef_ok(u[i]);
     r.finite = fin;
     return r;
 }
@@ -866,7 +883,8 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue_lean(con
     r.grad_zero = u[ji(1, 0)] == 0.0 && u[ji(0, 1)] == 0.0;
     const double m = max_abs(max_abs(max_abs(u[ji(0, 0)], u[ji(1, 0)]), max_abs(u[ji(0, 1)], u[ji(2, 0)])),
                              u[ji(0, 2)]);
-    r.finite = isfinite(r.scale) && !isnan(u[ji(0, 0)]) && m < kHugeJet && m != 0.0;
+    // (bitwise: && would make the compiler branch around the later tests)
+    r.finite = isfinite(r.scale) & !isnan(u[ji(0, 0)]) & (m < kHugeJet) & (m != 0.0);
     return r;
 }
 
@@ -898,7 +916,58 @@ __device__ __forceinline__ double scaled_fast(double res_abs, double S) {
     return scaled(res_abs, S);
 }
 
+// The grid's zero test without a division: a finite point fails tier 1 iff |res| > tau * S
+// (S >= 0 finite).  It equals fl(|res| / S) > tau except where |res| / S lies within a rounding
+// of tau (a tolerance either way); S == 0 fails iff res != 0, as scaled() gives inf there.  The
+// oracle (oracle/jet_oracle.c grid_fails) applies the same rule.
+__device__ __forceinline__ bool grid_fails(double res_abs, double S, double tau) { return res_abs > tau * S; }
+
+// a fast estimate of res / S (hardware reciprocal, no refinement): only ORDERS the grid points
+// of a lane for the running maximum of q (GridMax); the reported q is the IEEE quotient of the
+// point it chose
+__device__ __forceinline__ double q_estimate(double res_abs, double S) {
+#ifndef PD_HOST_SIM
+    return res_abs * __builtin_amdgcn_rcp(S);
+#else
+    return res_abs * (1.0 / S);
+#endif
+}
+
+// Per-lane running maximum of the scaled residual q = |res| / S over the finite grid points
+// without a division per point.  EXACT (Kerr, whose grid-reject text prints q_grid): the point
+// with the largest estimate is kept as the pair (|res|, S) and divided once at the end (q() is
+// scaled(), so q_grid is that point's IEEE quotient -- the old value wherever the estimates order
+// the points as the quotients do, i.e. unless two quotients of a lane agree to the estimate's
+// accuracy).  res == 0 with S == 0 (estimate NaN) never wins, as q = 0 there; S == 0 with
+// res > 0 (estimate inf) wins, q = inf.  !EXACT (force-free, whose q_grid no reason text
+// reads): the maximum of the estimates themselves, in one register pair instead of three.
+template <bool EXACT> struct GridMax {
+    double r = 0.0, s = 1.0, e = 0.0;
+    __device__ __forceinline__ void add(bool finite, double res_abs, double S) {
+        const double est = q_estimate(res_abs, S);
+        const bool take = finite & (est > e);
+        if constexpr (EXACT) {
+            r = take ? res_abs : r;
+            s = take ? S : s;
+        }
+        e = take ? est : e;
+    }
+    __device__ __forceinline__ double q() const {
+        if constexpr (EXACT) return scaled(r, s);
+        else return e;
+    }
+};
+
 // ------------------------------------------------------------------ wave reductions
+// the lanes where b holds (one s_and with exec of the compare's lane mask; HIP's __ballot(int)
+// first turns the bool into an int in a VGPR and compares it again: 2 VALU more per count)
+__device__ __forceinline__ int count_lanes(bool b) {
+#ifndef PD_HOST_SIM
+    return (int)__popcll(__builtin_amdgcn_ballot_w64(b));
+#else
+    return (int)__popcll(__ballot(b));
+#endif
+}
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -1118,7 +1187,8 @@ void validate_kernel(KernelArgs a) {
     if (a.list && nwork > a.list_capacity) nwork = a.list_capacity;
 
     for (int64_t wi = wave0; wi < nwork; wi = PERSISTENT ? wi + wstride : nwork) {
-        const int64_t cand = a.list ? (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]) : wi;
+        const int64_t cand = a.list ? checked_cand(a, (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]), ERRW_GENERIC) : wi;
+        if (cand < 0) continue;
         int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
         // programs are addressed relative to their first word with 32-bit offsets
         const bool in_bounds = beg >= 0 && end > beg && end <= a.n_words && end - beg < (1 << 24);
@@ -1216,7 +1286,7 @@ void validate_kernel(KernelArgs a) {
             {
                 const bool g = active && p >= a.n_ref;
                 nfin += (int)__popcll(__ballot(g && r.finite));
-                nbad += (int)__popcll(__ballot(g && r.finite && qv > a.prm.tau_grid));
+                nbad += (int)__popcll(__ballot(g && r.finite && grid_fails(r.res_abs, r.scale, a.prm.tau_grid)));
                 nnonfin += (int)__popcll(__ballot(g && !r.finite));
             }
             if (ch == 0) {

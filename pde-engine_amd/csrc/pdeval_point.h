@@ -314,7 +314,8 @@ __global__ __launch_bounds__(256, 1) void point_kernel(KernelArgs a) {
     LdsStack<double, NC> stk{vs, es, lane};
     const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= a.n) return;
-    const int64_t cand = a.perm ? (int64_t)a.perm[li] : li;   // lanes take programs sorted by shape
+    const int64_t cand = a.perm ? checked_cand(a, (int64_t)a.perm[li], ERRW_PERM) : li;   // lanes take programs sorted by shape
+    if (cand < 0) return;
     int64_t beg, end;
     uint8_t ps = P0_NONE;
     if (prog_bounds(a, cand, &beg, &end)) {
@@ -362,9 +363,9 @@ __global__ __launch_bounds__(64, 1) void point_list_kernel(KernelArgs a) {
     PrivStack<T, nc(K), MAXD - 1> stk;
     for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwork;
          wi += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t cand = a.list[wi];
+        const int64_t cand = checked_cand(a, a.list[wi], ERRW_POINT_LIST);
         int64_t beg, end;
-        if (!prog_bounds(a, cand, &beg, &end)) continue;   // pass 0 checked these
+        if (cand < 0 || !prog_bounds(a, cand, &beg, &end)) continue;   // pass 0 checked these
         const int32_t* prog = a.ops + beg;
         const uint32_t hdr = (uint32_t)prog[0];
         bool nf, perr;
@@ -410,7 +411,8 @@ template <int PROB, int MODE>
 __global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a) {
     const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (li >= a.n) return;
-    const int64_t cand = a.perm ? (int64_t)a.perm[li] : li;   // lists in shape order
+    const int64_t cand = a.perm ? checked_cand(a, (int64_t)a.perm[li], ERRW_PERM) : li;   // lists in shape order
+    if (cand < 0) return;
     const uint8_t ps = a.pstate[cand];
     if ((ps & 3) == P0_NONE) return;
     if (MODE == DD_EARLY) {
@@ -671,7 +673,8 @@ __global__ __launch_bounds__(64, MAXD == 2 ? PD_DD2_WAVES : 1) void dd_point_ker
     if constexpr (MAXD == 2) stk = STK{reinterpret_cast<T*>(pd_lds), (int)(threadIdx.x & 63)};
     for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwork;
          wi += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t cand = a.list[wi];
+        const int64_t cand = checked_cand(a, a.list[wi], ERRW_DD);
+        if (cand < 0) continue;
         int64_t beg, end;
         uint8_t s = P0_NONE;
         if (prog_bounds(a, cand, &beg, &end)) {
@@ -699,7 +702,9 @@ __global__ __launch_bounds__(256) void dd_apply_kernel(KernelArgs a) {
     const int64_t n2 = count(a.esc_count);
     for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < n0 + n1 + n2;
          wi += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t cand = wi < n0 ? a.defer_list[wi] : (wi < n0 + n1 ? a.cplx_list[wi - n0] : a.esc_list[wi - n0 - n1]);
+        const int64_t cand = checked_cand(
+            a, wi < n0 ? a.defer_list[wi] : (wi < n0 + n1 ? a.cplx_list[wi - n0] : a.esc_list[wi - n0 - n1]), ERRW_DD_APPLY);
+        if (cand < 0) continue;
         const uint8_t s = a.ddps[cand];
         if (s != kDdKeep) dd_apply_one(a, cand, s);
     }

@@ -473,7 +473,8 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
         const int64_t wi = wp / PARTS;
         const int part = (int)(wp - wi * PARTS);
         const int64_t entry = a.list[wi];
-        const int64_t cand = entry & PD_ESC_CAND_MASK;
+        const int64_t cand = checked_cand(a, entry < 0 ? -1 : (entry & PD_ESC_CAND_MASK), ERRW_TIER2);
+        if (cand < 0) continue;
         const uint32_t flags = (uint32_t)(entry >> PD_ESC_SHIFT);
         const int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
         const int32_t* prog = a.ops + beg;     // bounds were checked by pass 1
@@ -538,7 +539,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
                 const double qv = scaled(r.res_abs, r.scale);
                 qmax = fmax(qmax, qv);
                 if (!r.grad_zero) grad_nz = true;
-                if (qv > a.prm.tau_grid) {
+                if (grid_fails(r.res_abs, r.scale, a.prm.tau_grid)) {
                     ++nb1;
                     if (r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale, a.prm.omega2)) ++nb2;
                 }

@@ -153,12 +153,16 @@ def symbolic_zero_gradient(pd, items, out) -> List[int]:
                 (fp.max(axis=1) - fp.min(axis=1) <= 1e-9 * np.maximum(np.abs(fp).max(axis=1), 1e-300)) &
                 np.isin(st, (CLS_ACCEPT, CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC)))
     idx = np.flatnonzero(flat)
+    # each check has a time bound (SymPy's diff of a pathological tree has none of its own); one
+    # that hits it keeps the device's class
     if len(idx) and all(isinstance(items[i], str) for i in idx):
         # strings: over the SymPy pool when it runs, even one at a time (the caller's thread then
         # keeps the GIL free for the worker's other pipeline stages)
-        zero = hostpool.run(_zero_gradient_str, [(pd.slug, items[i]) for i in idx], min_items=1)
+        zero = hostpool.run(_zero_gradient_str, [(pd.slug, items[i]) for i in idx], min_items=1,
+                            item_timeout=HOST_CHECK_TIMEOUT_S, default=False)
     else:
-        zero = [_zero_gradient(pd, items[i]) for i in idx]
+        zero = [hostpool._call_bounded(lambda u: _zero_gradient(pd, u), items[i], HOST_CHECK_TIMEOUT_S, False)
+                for i in idx]
     rows = []
     for i, z in zip(idx.tolist(), zero):
         if z:
@@ -180,6 +184,9 @@ def _zero_gradient(pd, u) -> bool:
 
 
 _PDS: Dict[str, object] = {}
+# the time bound of one host SymPy check (zero gradient, the Kerr exact point check): the
+# reference's own check has none; past it the device's class stands
+HOST_CHECK_TIMEOUT_S = 30.0
 
 
 def _zero_gradient_str(args) -> bool:
@@ -233,7 +240,8 @@ def kerr_symbolic_constant(pd, items, out, ops, off) -> List[int]:
         keeps = hostpool.run(_kerr_keeps_coordinate_str, [(pd.slug, items[i]) for i in sel], min_items=1,
                     item_timeout=KERR_SIMPLIFY_TIMEOUT_S, default=None)
     else:
-        keeps = [_kerr_keeps_coordinate(pd, items[i]) for i in sel]
+        keeps = [hostpool._call_bounded(lambda u: _kerr_keeps_coordinate(pd, u), items[i],
+                                        KERR_SIMPLIFY_TIMEOUT_S, None) for i in sel]
     rows = []
     for i, k in zip(sel, keeps):
         if k:
@@ -421,18 +429,27 @@ def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-1
     with np.errstate(divide='ignore'):
         prm_pt = [Mv, av] + [float(np.float64(1.0) / np.float64(t)) for t in (Mv, av)] + [Mv * Mv, av * av] + \
                  [float(np.float64(1.0) / np.float64(t * t)) for t in (Mv, av)]
-    rows = []
+    sel = []
     for i in np.flatnonzero(a0_sel | ovf_sel):
         w = ops[off[i]:off[i + 1]]
         a0 = bool(a0_sel[i]) and _has_prm(w)
         ovf = bool(ovf_sel[i]) and _has_op(w, _EXP_OPS) and _exp_overflows(w, prm_pt)
-        if not (a0 or ovf):
-            continue
-        try:
-            u = items[i] if isinstance(items[i], sp.Basic) else pd.parse(items[i])
-            if not _kerr_fast_point_check(pd, kerr, u, abs_tol):
-                continue
-        except Exception:   # noqa: BLE001  (the device's reject stands)
+        if a0 or ovf:
+            sel.append(int(i))
+    if not sel:
+        return []
+    # the reference's 3-point check (SymPy diff + N(., 40)) per candidate, with a time bound
+    # (over the SymPy pool for strings); one that hits it, or fails, keeps the device's reject
+    kspec = (kerr.M_num, kerr.M_den, kerr.a_num, kerr.a_den, bool(kerr.op_M_fixed), bool(kerr.op_a_fixed))
+    if all(isinstance(items[i], str) for i in sel):
+        passes = hostpool.run(_kerr_point_check_str, [(pd.slug, kspec, items[i], abs_tol) for i in sel],
+                              min_items=1, item_timeout=HOST_CHECK_TIMEOUT_S, default=False)
+    else:
+        passes = [hostpool._call_bounded(lambda u: _kerr_point_check_safe(pd, kspec, u, abs_tol), items[i],
+                                         HOST_CHECK_TIMEOUT_S, False) for i in sel]
+    rows = []
+    for i, ok in zip(sel, passes):
+        if not ok:
             continue
         no_grid = int(out['n_nonfinite'][i]) >= n_grid
         st[i] = CLS_REJECT_GRID if (out['n_bad'][i] > max_bad or no_grid) else CLS_ACCEPT
@@ -442,15 +459,32 @@ def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-1
     return rows
 
 
-def _kerr_fast_point_check(pd, kerr, u, abs_tol) -> bool:
-    """kerr validator.py:77-91 (lhs) and :163-192 (the 3-point check) in SymPy."""
+def _kerr_point_check_safe(pd, kspec, u, abs_tol) -> bool:
+    try:
+        u = u if isinstance(u, sp.Basic) else pd.parse(u)
+        return _kerr_fast_point_check(pd, kspec, u, abs_tol)
+    except Exception:   # noqa: BLE001  (the device's reject stands)
+        return False
+
+
+def _kerr_point_check_str(args) -> bool:
+    slug, kspec, s, abs_tol = args
+    if slug not in _PDS:
+        _PDS[slug] = P.get(slug)
+    return _kerr_point_check_safe(_PDS[slug], kspec, s, abs_tol)
+
+
+def _kerr_fast_point_check(pd, kspec, u, abs_tol) -> bool:
+    """kerr validator.py:77-91 (lhs) and :163-192 (the 3-point check) in SymPy.  ``kspec`` =
+    (M_num, M_den, a_num, a_den, op_M_fixed, op_a_fixed) of the context's Kerr constants."""
+    M_num, M_den, a_num, a_den, op_M_fixed, op_a_fixed = kspec
     r, x = pd.x, pd.y
-    M = sp.Rational(kerr.M_num, kerr.M_den) if kerr.op_M_fixed else pd.constants['M']
-    a = sp.Rational(kerr.a_num, kerr.a_den) if kerr.op_a_fixed else pd.constants['a']
+    M = sp.Rational(M_num, M_den) if op_M_fixed else pd.constants['M']
+    a = sp.Rational(a_num, a_den) if op_a_fixed else pd.constants['a']
     G = 1 - (2 * M * r) / (r**2 + a**2 * x**2)
     lhs = sp.diff(G / (1 - x**2) * sp.diff(u, r), r) + sp.diff(G / (r**2 - 2 * M * r + a**2) * sp.diff(u, x), x)
-    base = {pd.constants['M']: sp.Rational(kerr.M_num, kerr.M_den),
-            pd.constants['a']: sp.Rational(kerr.a_num, kerr.a_den)}
+    base = {pd.constants['M']: sp.Rational(M_num, M_den),
+            pd.constants['a']: sp.Rational(a_num, a_den)}
     worst, n_ok = 0.0, 0
     for px, py in ((sp.Rational(5, 2), sp.Rational(3, 5)), (sp.Rational(7, 3), sp.Rational(1, 3)),
                    (sp.Integer(5), sp.Rational(-2, 5))):
@@ -468,7 +502,7 @@ def _kerr_fast_point_check(pd, kerr, u, abs_tol) -> bool:
     return n_ok > 0 and worst < abs_tol
 
 
-SYMBOLIC_MODES = ('off', 'text', 'replay')
+SYMBOLIC_MODES = ('off', 'strict', 'text', 'replay')
 SYMBOLIC_TIMEOUT_S = 60.0    # per candidate: the limit the reference fixtures were made with
 
 
@@ -497,10 +531,14 @@ def symbolic_stage(pd, items, out, mode: str = 'text', timeout: float = SYMBOLIC
     if mode == 'off':
         return []
     if pd.problem_id == PROBLEM_KERR:
+        if mode == 'strict':        # (the force-free symbolic stage's shapes; Kerr keeps 'off')
+            return []
         return _kerr_symbolic_stage(pd, items, out, mode, timeout, kerr)
     if pd.problem_id != PROBLEM_FORCE_FREE:
         return []
     st = np.asarray(out['status'])
+    if mode == 'strict':
+        return _strict_stage(pd, items, out, timeout, omega)
     cls = (CLS_REJECT_GRID, CLS_REJECT_SYMBOLIC) if mode == 'text' else (CLS_REJECT_GRID, CLS_ACCEPT, CLS_REJECT_SYMBOLIC)
     sel = np.flatnonzero(np.isin(st, cls)).tolist()
     if not sel:
@@ -525,6 +563,41 @@ def symbolic_stage(pd, items, out, mode: str = 'text', timeout: float = SYMBOLIC
         ok, text = r
         new = CLS_ACCEPT if ok else (CLS_REJECT_GRID if st[i] == CLS_REJECT_GRID else CLS_REJECT_SYMBOLIC)
         ov[i] = text
+        if new != st[i]:
+            st[i] = new
+            if 'verdict' in out:
+                out['verdict'][i] = bool(ok)
+        rows.append(i)
+    return rows
+
+
+def _strict_stage(pd, items, out, timeout, omega) -> List[int]:
+    """'strict': the grid zeros (ACCEPT, REJECT_SYMBOLIC) of a suspect shape
+    (pdeval.symbolic.suspect) get the reference's symbolic verdict and text; every other
+    candidate keeps the device's.  One pool task per grid zero: parse, shape test, and the
+    replay when suspect, under the per-candidate time bound (past it: the device's verdict).
+    ``out['strict']`` receives {'grid_zero', 'suspect', 'replayed', 'timeouts'}."""
+    st = np.asarray(out['status'])
+    sel = np.flatnonzero(np.isin(st, (CLS_ACCEPT, CLS_REJECT_SYMBOLIC))).tolist()
+    stats = out.setdefault('strict', {'grid_zero': 0, 'suspect': 0, 'replayed': 0, 'timeouts': 0})
+    stats['grid_zero'] += len(sel)
+    if not sel:
+        return []
+    args = [(pd.slug, items[i] if isinstance(items[i], str) else str(items[i]), omega) for i in sel]
+    res = hostpool.run(S.strict_str, args, min_items=1, item_timeout=timeout, default='timeout')
+    ov = out.setdefault('reason_override', {})
+    rows = []
+    for i, r in zip(sel, res):
+        if r == 'keep' or r is None:
+            continue
+        stats['suspect'] += 1
+        if r == 'timeout':
+            stats['timeouts'] += 1
+            continue
+        stats['replayed'] += 1
+        ok, text = r
+        ov[i] = text
+        new = CLS_ACCEPT if ok else CLS_REJECT_SYMBOLIC
         if new != st[i]:
             st[i] = new
             if 'verdict' in out:
@@ -573,6 +646,24 @@ def _kerr_symbolic_stage(pd, items, out, mode, timeout, kerr) -> List[int]:
     return rows
 
 
+def apply_host_steps(pd, kerr, params, n_grid: int, items, r, ops, off, symbolic: str = 'off',
+                     symbolic_timeout: float = SYMBOLIC_TIMEOUT_S, omega: str = '0'):
+    """The host steps every device result goes through (in place): the symbolic zero-gradient
+    re-check (force-free), the structural constant re-check of numeric constants with an Abs
+    or fractional power (Kerr), the reference's exact point check for Kerr values beyond the
+    fp64 range, and (``symbolic`` != 'off') the replay of the reference's symbolic stage.
+    ``r`` is one validate call's outputs (``status``, ``verdict``, ``res_ref``, ``q_ref``,
+    ``n_bad``, ``n_nonfinite``, ``fingerprint``); ``n_grid`` the grid's point count.  Needs no
+    GPU: the multi-rank path runs it per shard before the gather (pdeval.shard.final_verdicts)."""
+    symbolic_zero_gradient(pd, items, r)
+    kerr_symbolic_constant(pd, items, r, ops, off)
+    kerr_exact_point_check(pd, kerr, items, r, ops, off, params.kerr_abs_tol, n_grid, bool(params.full_grid),
+                           int(params.max_bad))
+    if symbolic != 'off' and (params.full_grid or pd.problem_id == PROBLEM_KERR):
+        symbolic_stage(pd, items, r, symbolic, symbolic_timeout, kerr, omega=omega)
+    return r
+
+
 class BatchValidator:
     """One problem on one GPU.  Thread-safe (calls are serialized per context).
 
@@ -619,22 +710,12 @@ class BatchValidator:
 
     def host_steps(self, r, ops, off, items, symbolic: Optional[str] = None,
                    symbolic_timeout: Optional[float] = None):
-        """The host steps every device result goes through (in place): the symbolic
-        zero-gradient re-check (force-free), the structural constant re-check of numeric
-        constants with an Abs or fractional power (Kerr), the reference's exact point check
-        for Kerr values beyond the fp64 range, and (force-free, ``symbolic`` != 'off') the
-        replay of the reference's symbolic stage."""
-        symbolic_zero_gradient(self.pd, items, r)
-        kerr_symbolic_constant(self.pd, items, r, ops, off)
-        kerr_exact_point_check(self.pd, self.kerr, items, r, ops, off, self.params.kerr_abs_tol,
-                               self.ctx.n_points - self.ctx.n_ref, bool(self.params.full_grid),
-                               int(self.params.max_bad))
-        mode = self.symbolic if symbolic is None else symbolic
-        if mode != 'off' and (self.params.full_grid or self.problem_id == PROBLEM_KERR):
-            symbolic_stage(self.pd, items, r, mode,
-                           self.symbolic_timeout if symbolic_timeout is None else symbolic_timeout, self.kerr,
-                           omega=self.omega)
-        return r
+        """The host steps every device result goes through (in place): :func:`apply_host_steps`
+        with this validator's problem, constants and mode."""
+        return apply_host_steps(self.pd, self.kerr, self.params, self.ctx.n_points - self.ctx.n_ref, items, r,
+                                ops, off, self.symbolic if symbolic is None else symbolic,
+                                self.symbolic_timeout if symbolic_timeout is None else symbolic_timeout,
+                                self.omega)
 
     def table(self, r, ops, off, notes) -> dict:
         """Device result (after host_steps) -> {'ok': bool array, 'reasons': list of str} plus

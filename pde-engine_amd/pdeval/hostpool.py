@@ -19,7 +19,10 @@ replacement from the parent -- by then GPU-live -- whenever a child exits): if a
 are computed in-process, and every later call runs in-process.  Children never touch the GPU.
 A per-item time bound (``run(..., item_timeout=s, default=d)``) is enforced inside the child
 with SIGALRM (raised as a ``BaseException`` SymPy cannot swallow); the item then yields
-``default``.
+``default``.  The job as a whole has a deadline too (a child stuck in a C-level call ignores the
+signal): chunks still missing then yield ``default``.  In-process, the bound is SIGALRM on the
+main thread and an abandoned helper thread elsewhere, so no bounded call can stall a worker
+thread past its bound.
 """
 from __future__ import annotations
 
@@ -29,11 +32,13 @@ import queue as _queue
 import signal
 import sys
 import threading
+import time
 from typing import List, Optional, Sequence
 
 import numpy as np
 
 _POOL = None
+DEADLINE_MARGIN_S = 30.0     # map_chunks: slack of a bounded job's deadline beyond its items' bounds
 
 
 class _ItemTimeout(BaseException):
@@ -56,18 +61,52 @@ def _gpu_live() -> bool:
 
 
 def _call_bounded(fn, x, item_timeout, default):
-    """fn(x), or ``default`` after ``item_timeout`` seconds (main thread only: SIGALRM)."""
-    if not item_timeout or threading.current_thread() is not threading.main_thread():
+    """fn(x), or ``default`` after ``item_timeout`` seconds.  On the main thread the bound is
+    SIGALRM (raised as ``_ItemTimeout``, a BaseException SymPy cannot swallow); the previous
+    SIGALRM handler and interval timer are restored afterwards.  On any other thread (the
+    worker's pipeline threads, when the pool is not running) fn runs on a helper daemon thread
+    that is abandoned at the bound: the caller gets ``default`` in time, and the abandoned
+    call finishes (or not) on its own without holding anything the caller needs."""
+    if not item_timeout:
         return fn(x)
+    if threading.current_thread() is not threading.main_thread():
+        return _call_on_thread(fn, x, item_timeout, default)
     old = signal.signal(signal.SIGALRM, _alarm)
-    signal.setitimer(signal.ITIMER_REAL, float(item_timeout))
+    prev = signal.setitimer(signal.ITIMER_REAL, float(item_timeout))
     try:
-        return fn(x)
+        try:
+            r = fn(x)
+        finally:
+            # disarmed inside the try: a timer that fires between fn's return and here still
+            # lands in the handler below, never in the caller
+            signal.setitimer(signal.ITIMER_REAL, 0)
+        return r
     except _ItemTimeout:
         return default
     finally:
-        signal.setitimer(signal.ITIMER_REAL, 0)
         signal.signal(signal.SIGALRM, old)
+        if prev[0] > 0:
+            signal.setitimer(signal.ITIMER_REAL, *prev)
+
+
+def _call_on_thread(fn, x, item_timeout, default):
+    box = []
+
+    def body():
+        try:
+            box.append((True, fn(x)))
+        except BaseException as e:   # noqa: BLE001  (re-raised in the caller)
+            box.append((False, e))
+
+    t = threading.Thread(target=body, daemon=True, name='pdeval-bounded')
+    t.start()
+    t.join(float(item_timeout))
+    if not box:
+        return default
+    ok, v = box[0]
+    if not ok:
+        raise v
+    return v
 
 
 def _child(tasks, results):
@@ -83,7 +122,12 @@ def _child(tasks, results):
             return
         job, k, fn, items, item_timeout, default = msg
         try:
-            out = [_call_bounded(fn, x, item_timeout, default) for x in items]
+            out = []
+            for x in items:
+                try:
+                    out.append(_call_bounded(fn, x, item_timeout, default))
+                except _ItemTimeout:     # (a late timer: the item counts as timed out)
+                    out.append(default)
             results.put((job, k, True, out))
         except Exception as e:   # noqa: BLE001  (the parent recomputes the chunk in-process)
             results.put((job, k, False, repr(e)))
@@ -103,6 +147,7 @@ class _FixedPool:
         for p in self.procs:
             p.start()
         self.broken = False
+        self.overdue = 0                     # jobs that hit their deadline (map_chunks)
         self.job = 0
         self.lock = threading.Lock()
         self.inbox = {}                      # job -> queue.Queue of (k, ok, out)
@@ -128,7 +173,16 @@ class _FixedPool:
 
     def map_chunks(self, fn, chunks, item_timeout=None, default=None) -> list:
         """Per chunk: its result list, or None where the pool could not deliver it (a child
-        died, or fn raised in the child); the caller computes those in-process."""
+        died, or fn raised in the child); the caller computes those in-process.  With an
+        ``item_timeout`` the whole job has a deadline (every item at its bound, spread over the
+        children, plus the longest chunk and a margin): a chunk still missing then -- a child
+        stuck in a C-level call that SIGALRM cannot interrupt -- yields ``default`` per item
+        (the device's verdict stands) instead of blocking the caller."""
+        deadline = None
+        if item_timeout:
+            n_items = sum(len(c) for c in chunks)
+            longest = max((len(c) for c in chunks), default=0)
+            deadline = time.monotonic() + float(item_timeout) * (n_items / max(1, self.n) + longest) + DEADLINE_MARGIN_S
         with self.lock:
             if self.broken:
                 return [None] * len(chunks)
@@ -145,6 +199,9 @@ class _FixedPool:
                 except _queue.Empty:
                     if self.broken:
                         break
+                    if deadline is not None and time.monotonic() > deadline:
+                        self.overdue += 1
+                        return [got[k] if k in got else [default] * len(chunks[k]) for k in range(len(chunks))]
                     continue
                 got[k] = out if ok else None
             return [got.get(k) for k in range(len(chunks))]

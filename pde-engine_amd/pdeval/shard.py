@@ -8,16 +8,15 @@ packed verdict bitmaps are then assembled on every rank with a single all-gather
 through the C ABI (``pdeval_gather_bits``, RCCL over xGMI, :func:`gather_verdicts_native`) or
 through ``torch.distributed`` (:func:`gather_verdicts`; gloo in the CPU tests).
 
-The gathered bitmap is the DEVICE's verdict, before the host steps of ``pdeval.batch``
-(``BatchValidator.host_steps``: the symbolic zero-gradient re-check, the Kerr structural
-constant re-check and the Kerr exact point check).  Those steps change verdicts in BOTH
-directions: the zero-gradient and constant re-checks turn True into False, but the Kerr exact
-point check turns a device point reject into an accept where only fp64 range caused the reject
-(a_value = 0, exp beyond +-708 at a reference point).  So the gathered bitmap under-accepts
-such Kerr candidates relative to the plugin.  A caller that needs the plugin's verdicts runs
-the host steps on its own shard (they need the candidate strings) and gathers the re-packed
-bits after (:func:`pack_bits` of the host-stepped verdicts), as ``pdeval.worker`` does per
-batch.
+What is gathered is the PLUGIN's final verdict, not the device bitmap: the host steps of
+``pdeval.batch`` (``apply_host_steps``: the symbolic zero-gradient re-check, the Kerr
+structural constant re-check, the Kerr exact point check, the symbolic modes) change verdicts
+in BOTH directions -- the zero-gradient and constant re-checks turn True into False, the Kerr
+exact point check turns a device point reject into an accept where only the fp64 range caused
+it (a_value = 0, exp beyond +-708 at a reference point).  So every rank runs them on its own
+shard (:func:`final_verdicts`; they need the candidate strings, which every rank has) and the
+re-packed bits go into the one all-gather -- the reference's result is the plugin verdict of
+each candidate (``general_method_paper_reproduction.py:1768-1816``).
 """
 from __future__ import annotations
 
@@ -134,3 +133,44 @@ def gather_verdicts_native(ctx, local_bits, ranges: Sequence[Tuple[int, int]], s
     ctx.gather_bits(buf.data_ptr(), nbytes, out.data_ptr(), stream)
     torch.cuda.synchronize(local_bits.device)
     return assemble_bits(out.cpu().numpy(), ranges)
+
+
+def final_verdicts(pd, kerr, params, n_grid: int, items, r: dict, ops, off, keys=None,
+                   symbolic: str = 'off') -> np.ndarray:
+    """This rank's final (plugin) verdicts: the device outputs ``r`` of its shard (host
+    arrays) through ``pdeval.batch.apply_host_steps``; returns bool[n] (``r`` is updated in
+    place: ``status``, ``verdict``).
+
+    ``keys`` (optional, int[n]): a program id per candidate when the shard repeats programs (the
+    bench's tiled batch).  The host steps then run once per distinct program, on its first
+    occurrence, and the resulting class is given to every occurrence -- the device's outputs
+    are a function of the program alone (bench.py checks that duplicates agree)."""
+    from .batch import apply_host_steps
+    from .opcodes import CLS_ACCEPT
+    st = np.asarray(r['status'])
+    n = len(st)
+    if 'verdict' not in r:
+        r['verdict'] = st == CLS_ACCEPT
+    if keys is None:
+        apply_host_steps(pd, kerr, params, n_grid, items, r, ops, off, symbolic)
+        return np.asarray(r['verdict'], dtype=bool).copy()
+    keys = np.asarray(keys)
+    _, first, inv = np.unique(keys, return_index=True, return_inverse=True)
+    sub = {k: np.asarray(v)[first] for k, v in r.items() if isinstance(v, np.ndarray) and len(v) == n}
+    sub_ops, sub_off = _gather(ops, off, first)
+    apply_host_steps(pd, kerr, params, n_grid, [items[i] for i in first], sub, sub_ops, sub_off, symbolic)
+    st[:] = sub['status'][inv]
+    r['verdict'] = st == CLS_ACCEPT
+    return np.asarray(r['verdict'], dtype=bool).copy()
+
+
+def _gather(ops, off, idx):
+    """Packed programs idx[...] of a packed batch (pdeval.workload.gather_programs)."""
+    ops = np.asarray(ops)
+    off = np.asarray(off, dtype=np.int64)
+    idx = np.asarray(idx, dtype=np.int64)
+    lens = off[idx + 1] - off[idx]
+    new_off = np.zeros(len(idx) + 1, dtype=np.int64)
+    np.cumsum(lens, out=new_off[1:])
+    starts = np.repeat(off[idx] - new_off[:-1], lens) + np.arange(new_off[-1], dtype=np.int64)
+    return ops[starts].astype(np.int32), new_off

@@ -23,6 +23,9 @@ replay hits the bound keeps the device's verdict and text):
 
 * ``text``   -- for grid rejects: SymPy's det_M and its printed length choose the text
   (the verdict is already False: a det that is non-zero on the grid is non-zero);
+* ``strict`` -- the reference's symbolic verdict and text only for the grid zeros of the
+  shapes where it is known to differ from det == 0 (:func:`suspect`); the throughput mode with
+  the reference's verdicts on every decided depth-4 and depth-5 fixture row;
 * ``replay`` -- additionally, for every candidate the device accepts or rejects by a
   structural rule (REJECT_SYMBOLIC): the reference's whole symbolic stage on SymPy's det_M,
   including the normalizer's 5 s wall-clock fallback to ``expand(det_M)``
@@ -171,7 +174,54 @@ def ff_point_stage(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol,
     return None if d < 1e-20 else (False, f'Invalid (point check ≈ {d:.2e})')
 
 
+# ------------------------------------------------------------------ 'strict': targeted replay
+def suspect(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol) -> bool:
+    """The shapes in which the reference's symbolic stage disagrees with det == 0 on the grid,
+    or in which the structural rules (NONSMOOTH2D, UNPROVABLE) stand in for it -- the only
+    candidates the 'strict' mode replays (fitted to every decided depth-4
+    and depth-5 reference row):
+      * an Abs anywhere (SymPy's Abs of real expressions: sqrt(square(.)), ((.)**2)**(p/2));
+      * a fractional power of a power (sqrt(1/(1 - z)), ((.)**2)**(3/2)) or of an exp
+        (exp(g)**(9/4));
+      * inside an exp, a fractional power whose base also occurs on its own
+        (exp(sqrt(rho/z) - rho/z): expand keeps sqrt(rho/z) and rho/z apart).
+    Every other grid zero keeps the device's verdict."""
+    for e in sp.preorder_traversal(u):
+        if isinstance(e, sp.Abs):
+            return True
+        if isinstance(e, sp.Pow) and not e.exp.is_Integer and e.base.has(rho, z):
+            if isinstance(e.base, (sp.Pow, sp.exp, sp.Abs)):
+                return True
+        if isinstance(e, sp.exp):
+            arg = e.args[0]
+            for f in sp.preorder_traversal(arg):
+                if isinstance(f, sp.Pow) and not f.exp.is_Integer and f.base.has(rho, z):
+                    b = f.base
+                    if sum(1 for g in sp.preorder_traversal(u) if g == b) >= 2:
+                        return True
+    return False
+
+
 _PDS: Dict[str, object] = {}
+
+
+def strict_str(args) -> Optional[Tuple[bool, str]]:
+    """'strict' mode for one grid-zero candidate string, in a SymPy pool process:
+    ``(slug, expr_str[, Omega])`` -> the reference's symbolic verdict and text if the candidate
+    is :func:`suspect`, else ``'keep'`` (the device's verdict stands); None if SymPy fails."""
+    slug, s = args[:2]
+    omega = sp.sympify(args[2]) if len(args) > 2 else sp.Integer(0)
+    from . import problem_defs as P
+    if slug not in _PDS:
+        _PDS[slug] = P.get(slug)
+    pd = _PDS[slug]
+    try:
+        u = pd.parse(s)
+        if not suspect(u, pd.x, pd.y):
+            return 'keep'
+    except Exception:   # noqa: BLE001
+        return None
+    return ff_replay(u, pd.x, pd.y, True, omega)
 
 
 def replay_str(args) -> Optional[Tuple[bool, str]]:

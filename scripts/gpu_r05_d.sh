@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 5, session d: the build with checked work-list reads (a list entry outside the batch is
+# reported by the call, not followed): the GPU tests, then the default bench.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${TAG:-r05_d}
+timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest_gpu.log 2>&1
+rc=$?; echo "PYTEST_RC=$rc"; [ $rc -eq 0 ] || exit 4
+timeout -k 10 900 python bench.py > gpurun_out/${T}_bench.log 2> gpurun_out/${T}_bench.err || exit 5
+echo ALL_RC=0

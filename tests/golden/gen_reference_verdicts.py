@@ -172,6 +172,7 @@ def main():
     ap.add_argument('--depth', type=int, default=None, help='only candidates of this depth')
     ap.add_argument('--sample', type=int, default=0, help='seeded sample size (0 = all)')
     ap.add_argument('--start', type=int, default=0, help='skip the first START input rows')
+    ap.add_argument('--stop', type=int, default=0, help='input rows before STOP only (0 = all)')
     ap.add_argument('--evidence', action='store_true', help="also record the validator's last_evidence()")
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--timeout', type=int, default=60)
@@ -222,7 +223,7 @@ def main():
     else:
         with open(a.input) as f:
             items = [(i, 0, l.strip()) for i, l in enumerate(f) if l.strip()]
-    items = items[a.start:]
+    items = items[a.start:a.stop] if a.stop else items[a.start:]
     if a.depth is not None:
         items = [it for it in items if it[1] == a.depth]
     if a.sample and a.sample < len(items):

@@ -225,3 +225,82 @@ def test_small_batch_graph_path_equals_direct():
     finally:
         g.close()
         d.close()
+
+
+def _ctx_with_env(problem_id, env, **kw):
+    """A Context created with the given PDEVAL_* environment (read once, at pdeval_create)."""
+    from pdeval._lib import Context
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return Context(problem_id, device=0, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def test_small_batch_graph_after_set_kerr_constants():
+    """A captured small-batch graph holds the Kerr constants by value; pdeval_set_kerr_constants
+    must drop it.  Validate <= 64 candidates, change the constants, validate again: the outputs
+    equal those of a fresh context built with the new constants and of one with PDEVAL_GRAPH=0."""
+    from pdeval import problem_defs as P
+    from pdeval import _lib
+    from pdeval.workload import gather_programs
+    pd_ = P.kerr()
+    kc_a, _ = G.KERR_CONFIGS['a=1/10']
+    kc_b, files_b = G.KERR_CONFIGS['a_value=0']
+    strs = [r['expr'] for r in G.ref_rows(*files_b)][:400]
+    ops, off, _ = P.compile_strings(pd_, strs)
+    g = _ctx_with_env(pd_.problem_id, {}, kerr=_lib.KerrConstants(*kc_a))
+    fresh = _ctx_with_env(pd_.problem_id, {}, kerr=_lib.KerrConstants(*kc_b))
+    direct = _ctx_with_env(pd_.problem_id, {'PDEVAL_GRAPH': '0'}, kerr=_lib.KerrConstants(*kc_b))
+    try:
+        changed = 0
+        for start, n in ((0, 64), (64, 1), (100, 37)):
+            idx = (start + np.arange(n)) % len(strs)
+            o, f = gather_programs(ops, off, idx)
+            g.set_kerr_constants(_lib.KerrConstants(*kc_a))
+            before = g.validate(o, f)                      # captures / replays the a = 1/10 graph
+            g.set_kerr_constants(_lib.KerrConstants(*kc_b))
+            a, b, c = g.validate(o, f), fresh.validate(o, f), direct.validate(o, f)
+            changed += int(np.any(before['res_ref'] != a['res_ref']))
+            for k in ('status', 'verdict', 'q_ref', 'res_ref', 'q_grid', 'n_bad', 'n_nonfinite', 'fingerprint'):
+                x = np.asarray(a[k])
+                assert np.array_equal(x, np.asarray(b[k]), equal_nan=x.dtype.kind == 'f'), (n, k, 'fresh')
+                assert np.array_equal(x, np.asarray(c[k]), equal_nan=x.dtype.kind == 'f'), (n, k, 'direct')
+        assert changed, 'the constants change the reference-point residuals'
+    finally:
+        g.close()
+        fresh.close()
+        direct.close()
+
+
+@pytest.mark.parametrize('n', [1023, 1024, 4096])
+def test_dd_early_split_equals_single_tier(n):
+    """The double-double tier beside the grid (PDEVAL_DD_EARLY=1: the P0_DD lists on a side
+    stream, dd_apply_kernel after the join) gives exactly the outputs of the single tier after
+    the grid (PDEVAL_DD_EARLY=0), at sizes on both sides of where the early path starts (1,024)
+    and where the small-batch row split ends."""
+    from pdeval import problem_defs as P
+    from pdeval.workload import gather_programs
+    pd_ = P.force_free()
+    strs = [r['expr'] for r in G.ref_rows('ff_d4_s2000.jsonl', 'ff_d4_s500.jsonl', 'ff_edge.jsonl', 'ff_d3_s500.jsonl')]
+    ops, off, _ = P.compile_strings(pd_, strs)
+    idx = np.random.default_rng(n).permutation(np.resize(np.arange(len(strs)), n))
+    o, f = gather_programs(ops, off, idx)
+    e1 = _ctx_with_env(pd_.problem_id, {'PDEVAL_DD_EARLY': '1'})
+    e0 = _ctx_with_env(pd_.problem_id, {'PDEVAL_DD_EARLY': '0'})
+    try:
+        a, b = e1.validate(o, f), e0.validate(o, f)
+        da, db = _device_outputs(e1, o, f, e1.n_ref), _device_outputs(e0, o, f, e0.n_ref)
+        for k in ('status', 'verdict', 'q_ref', 'res_ref', 'q_grid', 'n_bad', 'n_nonfinite', 'fingerprint'):
+            x = np.asarray(a[k])
+            assert np.array_equal(x, np.asarray(b[k]), equal_nan=x.dtype.kind == 'f'), (n, k)
+            assert np.array_equal(da[k], db[k], equal_nan=da[k].dtype.kind == 'f'), (n, k, 'device')
+        assert np.array_equal(da['status'], np.asarray(a['status']))
+    finally:
+        e1.close()
+        e0.close()

@@ -84,3 +84,78 @@ def test_two_rank_gather_equals_single_rank(tmp_path):
         got = np.load(tmp_path / f'rank{r}.npy')
         assert np.array_equal(got, single), r
     assert single.any() and not single.all()
+
+
+DEVICE_ROWS = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'device')
+
+
+def _device_rows(case):
+    """The device's raw outputs for fixture rows, recorded on the MI355X
+    (tests/golden/gen_device_outputs.py): the per-rank device results of this CPU test."""
+    z = np.load(os.path.join(DEVICE_ROWS, f'{case}.npz'), allow_pickle=False)
+    r = {k: z[k] for k in ('status', 'verdict', 'q_ref', 'res_ref', 'q_grid', 'n_bad', 'n_nonfinite', 'fingerprint')}
+    return str(z['problem']), [float(v) for v in z['kerr']], [str(s) for s in z['strings']], z['ops'], z['off'], r, z['ref_ok']
+
+
+def _kerr_of(pid, kerr):
+    from pdeval import _lib
+    if pid != 1:
+        return None
+    if kerr:
+        k = [int(v) for v in kerr[:4]] + [kerr[4], kerr[5]] + [int(v) for v in kerr[6:]]
+        return _lib.KerrConstants(*k)
+    return _lib.default_kerr_constants()
+
+
+def _final_rank_main(rank, world, port, case, out_dir):
+    import torch
+    import torch.distributed as dist
+    from pdeval import _lib
+    from pdeval.shard import final_verdicts, _gather
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        problem, kerr, strs, ops, off, r, _ = _device_rows(case)
+        pd_ = P.get(problem)
+        ranges = shard_ranges(len(strs), world)
+        s, e = ranges[rank]
+        sub = {k: v[s:e].copy() for k, v in r.items()}
+        o, f = _gather(ops, off, np.arange(s, e))
+        fin = final_verdicts(pd_, _kerr_of(pd_.problem_id, kerr), _lib.default_params(pd_.problem_id), 4096,
+                             strs[s:e], sub, o, f)
+        allv = gather_verdicts(torch.from_numpy(pack_bits(fin)), ranges)
+        np.save(os.path.join(out_dir, f'{case}_rank{rank}.npy'), allv)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('case', ['kerr_a_value0', 'kerr_d4_range', 'ff_edge_d2'])
+def test_two_rank_gather_of_final_verdicts(case, tmp_path):
+    """every rank runs the host steps on its own shard of device results
+    (pdeval.shard.final_verdicts) and the re-packed FINAL bits are what the all-gather carries.
+    With device outputs recorded on the MI355X (tests/golden/gen_device_outputs.py) -- Kerr at
+    a_value = 0, where the exact point check re-decides fp64-range point rejects; the Kerr
+    depth-4 rows whose class the host steps decide; the force-free symbolic zero-gradient row --
+    world 2 on gloo gives exactly the single-process plugin's verdicts (the same host steps over
+    the whole batch), which equal the reference's on every decided row, while the raw device
+    bitmap does not (force-free)."""
+    import torch.multiprocessing as mp
+    from pdeval import _lib
+    from pdeval.shard import final_verdicts
+    problem, kerr, strs, ops, off, r, ref_ok = _device_rows(case)
+    pd_ = P.get(problem)
+    raw = r['verdict'].astype(bool).copy()
+    fin = {k: v.copy() for k, v in r.items()}
+    single = final_verdicts(pd_, _kerr_of(pd_.problem_id, kerr), _lib.default_params(pd_.problem_id), 4096, strs,
+                            fin, ops, off)
+    mp.spawn(_final_rank_main, args=(2, _free_port(), case, str(tmp_path)), nprocs=2, join=True)
+    for k in range(2):
+        assert np.array_equal(np.load(tmp_path / f'{case}_rank{k}.npy'), single), k
+    dec = ref_ok >= 0
+    assert np.array_equal(single[dec], ref_ok[dec] == 1), [strs[i] for i in np.flatnonzero(dec & (single != (ref_ok == 1)))][:5]
+    if case == 'kerr_a_value0':
+        # the exact point check re-decides fp64-range point rejects (class changes; at these
+        # constants the grid then rejects them too, so the bits stay)
+        assert int((fin['status'] != r['status']).sum()) >= 3
+    if case == 'ff_edge_d2':
+        assert int((raw & ~single).sum()) >= 1                     # the symbolic zero gradient

@@ -147,3 +147,72 @@ def test_kerr_text_and_evidence(name, spec):
         elif ev != r['evidence']:
             bad.append((r['expr'], 'evidence'))
     assert not bad, bad[:3]
+
+
+def _ff_decided_fixture_rows():
+    rows = {}
+    for name in sorted(os.listdir(os.path.join(G.GOLDEN, 'ref'))):
+        if not name.startswith('ff_') or not name.endswith('.jsonl'):
+            continue
+        for r in G.decided(G.ref_rows(name)):
+            if r.get('omega', '0') == '0':
+                rows.setdefault(r['expr'], r)
+    return list(rows.values())
+
+
+def test_strict_mode_every_decided_row():
+    """'strict' (VERDICT r4 item 1): the device's class (the oracle's, equal class for class on
+    the GPU), then for the grid zeros of a suspect shape (pdeval.symbolic.suspect) the
+    reference's symbolic verdict -- the product's replay, recorded by scripts/replay_fixtures.py
+    -- gives the reference's verdict on EVERY decided force-free fixture row, depth 1 to 5
+    (bar replays past the time bound, which keep the device's verdict and are counted); the
+    default mode differs exactly on the rows golden_data lists.  Also reports the suspect
+    fraction of the grid zeros."""
+    import oracle_lib as O
+    pd = P.force_free()
+    rows = _ff_decided_fixture_rows()
+    strs = [r['expr'] for r in rows]
+    ops, off, _ = P.compile_strings(pd, strs)
+    ora = O.validate_mt(0, ops, off)
+    from pdeval.batch import symbolic_zero_gradient
+    symbolic_zero_gradient(pd, strs, ora)           # (the host step every result goes through)
+    rep = _replay_rows()
+    zero = np.isin(ora['status'], (CLS_ACCEPT, CLS_REJECT_SYMBOLIC))
+    n_suspect = n_timeout = 0
+    bad_strict, bad_off = [], []
+    for i, r in enumerate(rows):
+        ok_dev = bool(ora['status'][i] == CLS_ACCEPT)
+        ok = ok_dev
+        if zero[i] and S.suspect(pd.parse(r['expr']), pd.x, pd.y):
+            n_suspect += 1
+            x = rep.get(r['expr'])
+            assert x is not None, r['expr']        # every decided symbolic-stage row is recorded
+            if x['timeout'] or x['ok'] is None:
+                n_timeout += 1
+            else:
+                ok = bool(x['ok'])
+        if ok != r['ok']:
+            bad_strict.append(r['expr'])
+        if ok_dev != r['ok']:
+            bad_off.append(r['expr'])
+    assert not bad_strict, bad_strict[:10]
+    assert n_timeout <= 3, n_timeout
+    # the default mode: exactly the known divergences (no allowance)
+    assert set(bad_off) <= G.FF_OFF_MODE_DIVERGENCE, sorted(set(bad_off) - G.FF_OFF_MODE_DIVERGENCE)
+    print(f'strict: {len(rows)} decided rows, {int(zero.sum())} grid zeros, {n_suspect} suspect')
+
+
+def test_strict_stage_host_step():
+    pd = P.force_free()
+    items = ['exp_neg(rho/z - sqrt(rho/z))',      # suspect (exp of a radical beside its base)
+             'rho**2*z',                          # not suspect: keeps the device's ACCEPT
+             'pow_neg_3_2(square(rho - z))',      # suspect (Abs): rule reject, reference accepts
+             'rho*z']                             # point reject: not a grid zero
+    st = np.array([CLS_ACCEPT, CLS_ACCEPT, CLS_REJECT_SYMBOLIC, CLS_REJECT_POINT], np.uint8)
+    out = {'status': st.copy(), 'verdict': st == CLS_ACCEPT}
+    rows = symbolic_stage(pd, items, out, 'strict', timeout=60)
+    assert sorted(rows) == [0, 2]
+    assert out['status'][0] == CLS_REJECT_SYMBOLIC and not out['verdict'][0]
+    assert out['status'][1] == CLS_ACCEPT and 1 not in out['reason_override']
+    assert out['status'][2] == CLS_ACCEPT and out['verdict'][2]
+    assert out['strict'] == {'grid_zero': 3, 'suspect': 2, 'replayed': 2, 'timeouts': 0}
