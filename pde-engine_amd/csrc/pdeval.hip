@@ -51,6 +51,23 @@ enum {
     L_DDL8 = 18,      // early ones (P0_DD, beside the grid passes on the side stream)
     PD_N_LISTS = 19
 };
+// after the list counters in d_counts: the device error word (KernelArgs::errw), then the work
+// queue heads of the persistent list kernels (KernelArgs::qhead), one per launch, zeroed with
+// the counters at the start of every launch chain
+enum { Q_PASS2 = 0, Q_CPLX, Q_T2, Q_T2_3, Q_T2_8, Q_T2_C, Q_T2_C8, Q_N };
+// The list passes' schedule (context fields, env at pdeval_create): list_queue 0 static (item
+// blockIdx.x, then + gridDim.x), or chunks of list_queue items from a work-queue head
+// (KernelArgs::qhead); list_parts waves per candidate at full size.  Measured
+// (profiles/r05_g_ab_*, 2^21): one item per atomic made Kerr pass 2 36 ms against 22 ms static
+// -- one counter for ~320 k items serializes -- and 4 parts per candidate 65 ms (every part
+// pays the accumulator's atomics and device-scope fences)
+#ifndef PD_LIST_QUEUE
+#define PD_LIST_QUEUE 0
+#endif
+#ifndef PD_LIST_PARTS
+#define PD_LIST_PARTS 1
+#endif
+constexpr int PD_COUNT_WORDS = PD_N_LISTS + 1 + Q_N;
 
 namespace {
 struct Grid {
@@ -69,6 +86,8 @@ struct pdeval_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool dd_early = true;
+    int list_queue = PD_LIST_QUEUE;   // list passes: 0 static schedule, k > 0 queue chunks of k items
+    int list_parts = PD_LIST_PARTS;   // list passes: waves per candidate at full size
     uint8_t* d_ddps = nullptr;      // the early tier's classes, capacity cap
     double ref_x[4] = {0, 0, 0, 0}, ref_y[4] = {0, 0, 0, 0};
     dd ref_xd[4] = {}, ref_yd[4] = {};   // the reference points as double-doubles
@@ -410,6 +429,8 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_LEAN_CPLX")) c->lean_cplx = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_GRAPH")) c->use_graph = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_DD_EARLY")) c->dd_early = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_LIST_QUEUE")) c->list_queue = std::max(0, atoi(v));
+    if (const char* v = getenv("PDEVAL_LIST_PARTS")) c->list_parts = std::min(16, std::max(1, atoi(v)));
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     if ((e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess)
@@ -429,7 +450,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
         return rc;
     }
     // the list counters and, after them, the device error word (KernelArgs::errw)
-    if ((e = hipMalloc(&c->d_counts, (PD_N_LISTS + 1) * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
+    if ((e = hipMalloc(&c->d_counts, PD_COUNT_WORDS * sizeof(int32_t))) != hipSuccess) return fail("hipMalloc", e);
     *out = c;
     return PDEVAL_OK;
 }
@@ -680,6 +701,24 @@ template <class T, int K, int MAXD> constexpr size_t tier2_lds() {
 #define PD_DD_EARLY_MIN_N 1024
 #endif
 
+// The entries of a work list checked in a pass of their own, before the hot list kernels
+// (pass 2, the complex pass) read them unchecked: an entry outside [0, n) sets `code` in the
+// error word and empties the list (the call then reports the error; no kernel follows the entry).
+__global__ __launch_bounds__(256) void sanitize_list_kernel(const int64_t* list, int32_t* count, int64_t cap,
+                                                            int64_t n, uint32_t* errw, uint32_t code) {
+    int64_t m = (int64_t)*count;
+    if (m > cap) m = cap;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = list[i];
+        bad = bad || c < 0 || c >= n;
+    }
+    if (bad) {
+        atomicOr(errw, code);
+        *count = 0;
+    }
+}
+
 // zeroes `words` 32-bit words (the list counters, a small batch's verdict bits) -- a kernel node
 // in the captured graphs rather than a memset node
 __global__ void zero_words_kernel(uint32_t* p, int64_t words) {
@@ -728,9 +767,17 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // (a kernel, not hipMemsetAsync: captured into the small-batch graphs, a memset node was
     // seen to leave these counters unzeroed on replay -- the stale counts of an earlier, larger
     // batch then sent the list passes to entries outside the batch, profiles/r05_e_pytest_gpu.log)
-    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, s, (uint32_t*)cnt, (int64_t)(PD_N_LISTS + 1));
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(64), 0, s, (uint32_t*)cnt, (int64_t)PD_COUNT_WORDS);
     HIPCHK(c, hipGetLastError());
     a.errw = (uint32_t*)(cnt + PD_N_LISTS);
+    auto queue = [&](KernelArgs b, int q) {   // a persistent list launch with its own work queue
+        if (c->list_queue > 0) {
+            b.qhead = (uint32_t*)(cnt + PD_N_LISTS + 1 + q);
+            b.qchunk = c->list_queue;
+        }
+        return b;
+    };
+    const int lparts = std::max(grid_parts(n), c->list_parts);
     constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
     constexpr bool FF = PROB == PDEVAL_PROBLEM_FORCE_FREE;
     constexpr int WPB = 4;  // waves (candidates) per 256-thread block of pass 1
@@ -750,7 +797,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         return b;
     };
     // (small batches: enough blocks for every (candidate, part) of the split grid passes)
-    const unsigned pgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(4 * blocks, n * grid_parts(n)), 8192);
+    const unsigned pgrid = (unsigned)std::min<int64_t>(std::max<int64_t>(4 * blocks, n * lparts), 8192);
     // list-driven point kernels (one candidate per lane): enough blocks for the rare lists
     const unsigned lgrid = (unsigned)std::min<int64_t>((n + 63) / 64, 2048);
     a.defer_list = c->d_list[L_DEFER];
@@ -839,8 +886,10 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // slots); what it does not take, the generic stack-3 kernel
     mark(3);
     if (dmax > 2) {
-        launch_grid_list(PROB, pgrid, s, follow(L_DEFER, L_DEFER2, L_ESC), c->d_list[L_SLOW2], cnt + L_SLOW2,
-                         grid_parts(n));
+        hipLaunchKernelGGL(sanitize_list_kernel, dim3(64), dim3(256), 0, s, c->d_list[L_DEFER], cnt + L_DEFER, c->cap, n,
+                           a.errw, (uint32_t)ERRW_GRID_LIST);
+        launch_grid_list(PROB, pgrid, s, queue(follow(L_DEFER, L_DEFER2, L_ESC), Q_PASS2), c->d_list[L_SLOW2],
+                         cnt + L_SLOW2, lparts);
         HIPCHK(c, hipGetLastError());
         hipLaunchKernelGGL((validate_kernel<PROB, double, 3, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
                            dim3(64), (stack_lds<double, K, 3>(1)), s, follow(L_SLOW2, L_DEFER2, L_ESC));
@@ -861,8 +910,10 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         // the lean interpreter in complex arithmetic over the decoded programs; what it does not
         // take (point stage undecided, malformed) the generic complex kernel drains
         if (c->lean_cplx) {
-            launch_grid_cplx(pgrid, s, follow(L_CPLX, L_CPLX_DEEP, L_ESC_C), c->d_list[L_SLOW_C], cnt + L_SLOW_C,
-                             grid_parts(n));
+            hipLaunchKernelGGL(sanitize_list_kernel, dim3(64), dim3(256), 0, s, c->d_list[L_CPLX], cnt + L_CPLX, c->cap,
+                               n, a.errw, (uint32_t)ERRW_CPLX);
+            launch_grid_cplx(pgrid, s, queue(follow(L_CPLX, L_CPLX_DEEP, L_ESC_C), Q_CPLX), c->d_list[L_SLOW_C],
+                             cnt + L_SLOW_C, lparts);
             HIPCHK(c, hipGetLastError());
             hipLaunchKernelGGL((validate_kernel<PROB, cplx, 2, true>), dim3((unsigned)std::min<int64_t>(blocks, 256)),
                                dim3(64), (stack_lds<cplx, K, 2>(1)), s, follow(L_SLOW_C, L_CPLX_DEEP, L_ESC_C));
@@ -883,7 +934,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         mark(6);
     }
     // tier 2 (pdeval_tier2.h): re-decide every tier-1 grid failure with error bounds, by stack
-    KernelArgs t = follow(L_ESC, L_ESC_DEEP, L_ESC);
+    KernelArgs t = queue(follow(L_ESC, L_ESC_DEEP, L_ESC), Q_T2);
     mark(7);
     // (PARTS waves per entry: pdeval_tier2.h)
     hipLaunchKernelGGL((tier2_kernel<PROB, double, 2, false, PD_T2_PARTS>), dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS, 8192)),
@@ -892,26 +943,26 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     mark(8);
     if (dmax > 2) {
         hipLaunchKernelGGL((tier2_kernel<PROB, double, 3, false, PD_T2_PARTS>), dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS, 4096)),
-                           dim3(64), (tier2_lds<double, K, 3>()), s, follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC));
+                           dim3(64), (tier2_lds<double, K, 3>()), s, queue(follow(L_ESC_DEEP, L_ESC_DEEP2, L_ESC), Q_T2_3));
         HIPCHK(c, hipGetLastError());
     }
     mark(9);
     if (dmax > 3) {
         hipLaunchKernelGGL((tier2_kernel<PROB, double, PDEVAL_MAX_STACK>), dim3((unsigned)std::min<int64_t>(n, 512)),
-                           dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, follow(L_ESC_DEEP2, -1, L_ESC));
+                           dim3(64), (tier2_lds<double, K, PDEVAL_MAX_STACK>()), s, queue(follow(L_ESC_DEEP2, -1, L_ESC), Q_T2_8));
         HIPCHK(c, hipGetLastError());
     }
     if constexpr (FF) {
         mark(10);
         hipLaunchKernelGGL((tier2_kernel<PROB, cplx, 4, false, PD_T2_PARTS_C>),
                            dim3((unsigned)std::min<int64_t>(n * PD_T2_PARTS_C, 4096)), dim3(64),
-                           (tier2_lds<cplx, K, 4>()), s, follow(L_ESC_C, L_ESC_C_DEEP, L_ESC_C));
+                           (tier2_lds<cplx, K, 4>()), s, queue(follow(L_ESC_C, L_ESC_C_DEEP, L_ESC_C), Q_T2_C));
         HIPCHK(c, hipGetLastError());
         // complex programs of stack 5..8: operand stack in private memory (161 KiB of LDS would
         // not fit)
         if (dmax > 4) {
             hipLaunchKernelGGL((tier2_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>), dim3((unsigned)std::min<int64_t>(n, 256)),
-                               dim3(64), 0, s, follow(L_ESC_C_DEEP, -1, L_ESC_C));
+                               dim3(64), 0, s, queue(follow(L_ESC_C_DEEP, -1, L_ESC_C), Q_T2_C8));
             HIPCHK(c, hipGetLastError());
         }
     } else {

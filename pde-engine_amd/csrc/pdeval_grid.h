@@ -374,8 +374,12 @@ template <class T, int K, int W, int MAXD> struct Lean {
     static __device__ __forceinline__ bool live(int c) { return !(NOMIX && c == MIX); }
     // LDS layout: the live coefficients only (Kerr: 5 of 6 -- an operand slot of W = 8 jets is
     // 20 KiB per wave instead of 24, which is what 8 waves per CU fit in 160 KiB)
-    static constexpr int NCL = NCJ - (NOMIX ? 1 : 0);
-    static __device__ __forceinline__ constexpr int lidx(int c) { return NOMIX && c > MIX ? c - 1 : c; }
+#ifndef PD_LDS_COMPACT
+#define PD_LDS_COMPACT 1
+#endif
+    static constexpr bool COMPACT = PD_LDS_COMPACT && NOMIX;
+    static constexpr int NCL = NCJ - (COMPACT ? 1 : 0);
+    static __device__ __forceinline__ constexpr int lidx(int c) { return COMPACT && c > MIX ? c - 1 : c; }
     static constexpr int SLOT = W * NCL * 64;   // T values per operand slot
     static constexpr bool RSLOT = PD_LEAN_RSLOT && MAXD == 3;   // operand slot 1 in registers (run below)
     static constexpr int LDS_SLOTS = RSLOT ? 1 : MAXD - 1;
@@ -1012,10 +1016,12 @@ __global__ __launch_bounds__(64, PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : PD_LIST
     double* stk = reinterpret_cast<double*>(pd_lds);
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
-    for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
+    WorkQueue q;
+    for (int64_t wp = q.first(a); wp < nwork * parts; wp = q.next(a, wp)) {
         const int64_t wi = wp / parts;
-        const int64_t cand = checked_cand(a, (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]), ERRW_GRID_LIST);
-        if (cand < 0) continue;
+        // (entries checked before the launch: sanitize_list_kernel -- a check here, in the loop,
+        // cost this kernel 112 B of spill)
+        const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
         grid_body<PROB, 3, double, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count, (int)(wp % parts), parts);
     }
 }
@@ -1038,10 +1044,11 @@ __global__ __launch_bounds__(64, PD_CPLX_WAVES_PER_SIMD) void grid_cplx_kernel(K
     cplx* stk = reinterpret_cast<cplx*>(pd_lds);
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
-    for (int64_t wp = blockIdx.x; wp < nwork * parts; wp += gridDim.x) {
+    WorkQueue q;
+    for (int64_t wp = q.first(a); wp < nwork * parts; wp = q.next(a, wp)) {
         const int64_t wi = wp / parts;
-        const int64_t cand = checked_cand(a, (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]), ERRW_CPLX);
-        if (cand < 0) continue;
+        // (entries checked before the launch: sanitize_list_kernel -- 432 B of spill otherwise)
+        const int64_t cand = (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]);
         grid_body<PDEVAL_PROBLEM_FORCE_FREE, 2, cplx, ROT>(a, cand, threadIdx.x & 63, stk, slow_list, slow_count,
                                                       (int)(wp % parts), parts);
     }

@@ -91,6 +91,32 @@ struct KernelArgs {
     // bit k = a work-list entry outside [0, n) met by kernel family k (checked_cand), which is
     // then skipped; the host turns a non-zero word into an error of the call
     uint32_t* errw;
+    // persistent list kernels: the head of their work queue (a zeroed counter per launch), or
+    // NULL for the static schedule (item blockIdx.x, then + gridDim.x)
+    uint32_t* qhead;
+    int qchunk;                 // items per grab of the work queue
+};
+
+// The work items of a persistent one-wave block: the static schedule (item blockIdx.x, then
+// + gridDim.x), or -- when the launch has a queue head -- chunks of a.qchunk consecutive items
+// taken with one atomic each (a wave that finishes early takes the next chunk).
+#ifndef PD_QUEUE
+#define PD_QUEUE 1
+#endif
+struct WorkQueue {
+    int64_t end = 0;   // end of the current chunk (queue mode)
+    __device__ __forceinline__ int64_t grab(const KernelArgs& a) {
+        uint32_t v = 0;
+        if ((threadIdx.x & 63) == 0) v = atomicAdd(a.qhead, (uint32_t)a.qchunk);
+        const int64_t b = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        end = b + a.qchunk;
+        return b;
+    }
+    __device__ __forceinline__ int64_t first(const KernelArgs& a) { return PD_QUEUE && a.qhead ? grab(a) : (int64_t)blockIdx.x; }
+    __device__ __forceinline__ int64_t next(const KernelArgs& a, int64_t wp) {
+        if (!PD_QUEUE || !a.qhead) return wp + gridDim.x;
+        return wp + 1 < end ? wp + 1 : grab(a);
+    }
 };
 
 // A candidate index read from a work list or the shape permutation, checked: an entry outside
@@ -100,8 +126,11 @@ enum : uint32_t {
     ERRW_PERM = 1u, ERRW_GRID_LIST = 2u, ERRW_GENERIC = 4u, ERRW_POINT_LIST = 8u, ERRW_DD = 16u,
     ERRW_DD_APPLY = 32u, ERRW_TIER2 = 64u, ERRW_CPLX = 128u
 };
+#ifndef PD_CHECK_LISTS
+#define PD_CHECK_LISTS 1
+#endif
 __device__ __forceinline__ int64_t checked_cand(const KernelArgs& a, int64_t cand, uint32_t code) {
-    if (cand >= 0 && cand < a.n) return cand;
+    if (!PD_CHECK_LISTS || (cand >= 0 && cand < a.n)) return cand;
     if (a.errw) atomicOr(a.errw, code);
     return -1;
 }
@@ -268,7 +297,16 @@ template <class T, int K> struct JetOps {
     // t = a * t in place: outputs in decreasing total degree; c_ij reads t_kl only for
     // (k,l) <= (i,j), and no other output of degree i+j reads t_ij, so overwriting is safe
     // (saves a jet of registers against a separate result)
+#ifndef PD_MUL_TMP
+#define PD_MUL_TMP 0
+#endif
     static PD_HD void mul(const J& a, J& t) {
+        if constexpr (PD_MUL_TMP) {   // (codegen variant: the product into a temporary, then copied)
+            J r;
+            jmul<T, K, K, K>(a.c, t.c, r.c);
+            t = r;
+            return;
+        }
 #pragma unroll
         for (int d = K; d >= 0; --d) {
 #pragma unroll

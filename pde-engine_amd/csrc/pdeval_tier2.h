@@ -469,7 +469,8 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
     if constexpr (!PRIV) stk = STK{vs, es, lane};
     int64_t nwork = (int64_t)(*a.list_count);
     if (nwork > a.list_capacity) nwork = a.list_capacity;
-    for (int64_t wp = blockIdx.x; wp < nwork * PARTS; wp += gridDim.x) {
+    WorkQueue q;
+    for (int64_t wp = q.first(a); wp < nwork * PARTS; wp = q.next(a, wp)) {
         const int64_t wi = wp / PARTS;
         const int part = (int)(wp - wi * PARTS);
         const int64_t entry = a.list[wi];

@@ -20,11 +20,13 @@ inline double __shfl_xor(double v, int, int) { return v; }
 inline int __shfl_xor(int v, int, int) { return v; }
 inline bool __any(bool v) { return v; }
 inline unsigned long long __ballot(bool v) { return v ? 1ull : 0ull; }
+inline unsigned long long __builtin_amdgcn_ballot_w64(bool v) { return v ? 1ull : 0ull; }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 inline double __builtin_amdgcn_rcp(double v) { return 1.0 / v; }   // (v_rcp_f64: ~1 ulp)
 inline void __builtin_amdgcn_sched_barrier(int) {}
 inline int atomicAdd(int32_t* p, int v) { int o = *p; *p += v; return o; }
+inline uint32_t atomicAdd(uint32_t* p, uint32_t v) { uint32_t o = *p; *p += v; return o; }
 inline uint32_t atomicOr(uint32_t* p, uint32_t v) { uint32_t o = *p; *p |= v; return o; }
 inline uint32_t atomicAnd(uint32_t* p, uint32_t v) { uint32_t o = *p; *p &= v; return o; }
 inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) {
