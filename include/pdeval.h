@@ -160,6 +160,9 @@ typedef struct pdeval_params {
                             else it is re-evaluated in double-double  */
     double omega2;       /* force-free: Omega^2 of rotating field lines, a constant
                             (validator.py:326-329); 0 = the problem path's Omega = 0  */
+    double omega2_lo;    /* its low part: Omega^2 = omega2 + omega2_lo as a double-double, so a
+                            rational Omega^2 that is no double (Omega = 1/3: 1/9) is carried to
+                            2^-106 in the point stage's second tier; 0 when Omega^2 is a double */
 } pdeval_params;
 
 /* Per-candidate outputs; any pointer may be NULL (not produced).  Host or device memory

@@ -102,7 +102,11 @@ static void w_horner(const double* h0, const double* F, double* out, int K) {
 #define CI I
 /* force-free Omega^2 (pdeval_params.omega2), set by oracle_validate / oracle_set_omega2 */
 static double OM2 = 0.0;
+/* its low part (pdeval_params.omega2_lo): Omega^2 = OM2 + OM2_LO, a double-double -- the quad
+ * point stage takes both, the f64 grid stages OM2 alone (as the device) */
+static double OM2_LO = 0.0;
 int oracle_set_omega2(double w) { OM2 = w; return 0; }
+int oracle_set_omega2_lo(double w) { OM2_LO = w; return 0; }
 
 #define S double
 #define FN(name) name##_r
@@ -368,6 +372,9 @@ static pt_result eval_point_q(int problem, const int32_t* w, int64_t nw, int k, 
         kerr_terms((double)x, (double)y, cp, 0, &dummy, &S2, (double)KC.opM_pt, (double)KC.opa_pt);
     }
     r.noise = (S2 - r.scale) * (EPSQ / NOISE_GAMMA) + EPSQ * r.scale;
+    /* an Omega^2 carried as a double-double (OM2_LO != 0) is off by up to 2^-106 relative: the
+     * determinant, bilinear in it through A and B, by up to 2^-104 of its scale */
+    if (problem == PDEVAL_PROBLEM_FORCE_FREE && OM2_LO != 0) r.noise += 0x1p-104 * r.scale;
     r.res_abs = (double)cabsq(res);
     r.res_re = (double)crealq(res);
     r.finite = fin && finiteq(crealq(res)) && finiteq(cimagq(res)) && isfinite(r.scale) && isfinite(r.noise);
@@ -416,7 +423,10 @@ int oracle_validate(int problem, const int32_t* ops, const int64_t* offsets, int
                     int64_t first, int64_t count) {
     double *px, *py;
     int nref;
-    if (prm) OM2 = problem == PDEVAL_PROBLEM_FORCE_FREE ? prm->omega2 : 0.0;
+    if (prm) {
+        OM2 = problem == PDEVAL_PROBLEM_FORCE_FREE ? prm->omega2 : 0.0;
+        OM2_LO = problem == PDEVAL_PROBLEM_FORCE_FREE ? prm->omega2_lo : 0.0;
+    }
     int npts = build_points(problem, &px, &py, &nref);
     int G = npts - nref;
     int fp[PDEVAL_FP_N] = {0};

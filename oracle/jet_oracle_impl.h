@@ -350,7 +350,7 @@ static S FN(ff_det)(const S* c, CT rho, int mag) {
         /* rotating field lines, constant Omega (validator.py:326-329): with w = Omega^2,
          * A = A_0 - w C,  C = rho^2 (u20 + u02) + rho u10;  B = (1 - w rho^2) B_0 -- the
          * partials of both written out (the device does it on jets, ff_rotate_A / _B) */
-        const CT w = (CT)OM2, x = rho, x2 = rho * rho;
+        const CT w = (CT)OM2 + (CT)OM2_LO, x = rho, x2 = rho * rho;   /* (f64: = OM2) */
         S Cr = 2 * x * (u20 + u02) + x2 * (u30 + u12) + u10 + x * u20;
         S Cz = x2 * (u21 + u03) + x * u11;
         S Crr = 2 * (u20 + u02) + 4 * x * (u30 + u12) + x2 * (u40 + u22) + 2 * u20 + x * u30;

@@ -508,6 +508,7 @@ extern "C" int pdeval_default_params(int problem_id, pdeval_params* p) {
     p->point_abs_tol = 1e-20;  // validator.py:389
     p->res_rel_acc = 1e-11;    // residuals reported to 1e-10 relative (BASELINE.json north star)
     p->omega2 = 0.0;           // force-free Omega = 0 (problems/__init__.py:83)
+    p->omega2_lo = 0.0;
     (void)problem_id;
     return PDEVAL_OK;
 }

@@ -633,6 +633,9 @@ struct PointResult {
 #ifndef PD_AFMA
 #define PD_AFMA 1
 #endif
+PD_HD bool om2_nz(double w) { return w != 0.0; }
+PD_HD bool om2_nz(dd w) { return w.hi != 0.0; }
+
 template <class T, bool MAG> struct FFEpi {
     // Everything is read straight from u's Taylor coefficients (no materialized copies of
     // p = u_rho, q = u_z), and each intermediate dies as soon as its Lie derivative is
@@ -662,14 +665,15 @@ template <class T, bool MAG> struct FFEpi {
 
     // rho: R = double, or dd in the double-double point tier; r0 = rcp(rho) (the grid passes
     // pass their row's correctly rounded 1/x from the host table, the same value)
-    template <class R> static PD_HD T eval(const T* u, R rho, double om2 = 0.0) { return eval_r(u, rcp(rho), rho, om2); }
+    // om2: Omega^2 as O = double, or dd in the double-double point tier (params.omega2_lo)
+    template <class R, class O = double> static PD_HD T eval(const T* u, R rho, O om2 = O{}) { return eval_r(u, rcp(rho), rho, om2); }
     template <class R> static PD_HD T eval_r(const T* u, R r0) { return eval_r(u, r0, r0, 0.0); }
-    template <class R> static PD_HD T eval_r(const T* u, R r0, R rho, double om2) {
+    template <class R, class O> static PD_HD T eval_r(const T* u, R r0, R rho, O om2) {
         const R r2 = r0 * r0;
         return eval_p(u, r0, r2, r2 * r0, rho, om2);
     }
     // r2 = r0 * r0, r3 = r2 * r0 (the lean grid passes hand in their row's wave-uniform copies)
-    template <class R> static PD_HD T eval_p(const T* u, R r0, R r2, R r3, R rho, double om2) {
+    template <class R, class O> static PD_HD T eval_p(const T* u, R r0, R r2, R r3, R rho, O om2) {
         // 1/rho jet in the rho direction: (-1)^i / rho^(i+1)
         const R ri[3] = {r0, r2 * (MAG ? 1.0 : -1.0), r3};
         T LA[3], LB[3];
@@ -694,7 +698,7 @@ template <class T, bool MAG> struct FFEpi {
                     A[ji(i, j)] = s + sgn(pr);
 #endif
                 }
-            if (om2 != 0.0) rotate_A(A, u, rho, om2);
+            if (om2_nz(om2)) rotate_A(A, u, rho, om2);
             lie1(u, A, LA);
         }
         {
@@ -735,7 +739,7 @@ template <class T, bool MAG> struct FFEpi {
                     B[ji(i, j)] = s;
                 }
 #endif
-            if (om2 != 0.0) rotate_B(B, rho, om2);
+            if (om2_nz(om2)) rotate_B(B, rho, om2);
             lie1(u, B, LB);
         }
         // L_T^2 f (order 0) = q (L_T f)_rho - p (L_T f)_z
@@ -748,7 +752,7 @@ template <class T, bool MAG> struct FFEpi {
 
     // A -= om2 C, C = rho^2 (u_rr + u_zz) + rho u_r, order 2 in (rho, z); the rho^k factors as
     // jets in the rho direction: rho = (x, 1), rho^2 = (x^2, 2x, 1)
-    template <class R> static PD_HD void rotate_A(T* A, const T* u, R x, double om2) {
+    template <class R, class O> static PD_HD void rotate_A(T* A, const T* u, R x, O om2) {
         T PQ[6];
 #pragma unroll
         for (int d = 0; d <= 2; ++d)
@@ -772,7 +776,7 @@ template <class T, bool MAG> struct FFEpi {
             }
     }
     // B (1 - om2 rho^2)
-    template <class R> static PD_HD void rotate_B(T* B, R x, double om2) {
+    template <class R, class O> static PD_HD void rotate_B(T* B, R x, O om2) {
         T B0[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) B0[k] = B[k];

@@ -53,6 +53,19 @@ template <> __device__ __forceinline__ dd ref_coord<dd>(const KernelArgs& a, int
     return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3]));
 }
 
+// force-free Omega^2 as the coordinate type V: the double omega2, or omega2 + omega2_lo (a
+// rational Omega^2 that is no double, Omega = 1/3) -- and the bound, relative to the residual's
+// scale S, of what that representation error moves the determinant (bilinear in Omega^2 through
+// A and B: twice its relative error, doubled for margin; dd: 2^-106 relative, well under the
+// double-double noise unit)
+template <class V> __device__ __forceinline__ V om2_of(const KernelArgs& a);
+template <> __device__ __forceinline__ double om2_of<double>(const KernelArgs& a) { return a.prm.omega2; }
+template <> __device__ __forceinline__ dd om2_of<dd>(const KernelArgs& a) { return {a.prm.omega2, a.prm.omega2_lo}; }
+template <class V> __device__ __forceinline__ double om2_err(const KernelArgs& a) {
+    if (a.prm.omega2_lo == 0.0) return 0.0;
+    return std::is_same<V, dd>::value ? 0x1p-104 : 4.0 * fabs(a.prm.omega2_lo / a.prm.omega2);
+}
+
 // Kerr operator coefficients at reference point k, double-double (selects, as ref_coord)
 __device__ __forceinline__ void kc_ref_at(const KernelArgs& a, int k, dd (&kc)[4]) {
 #pragma unroll
@@ -111,7 +124,7 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
     const double* kc = a.kc ? a.kc + 4 * k : nullptr;
     T res;
     if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-        res = FFEpi<T, false>::eval(u.c, x, a.prm.omega2);
+        res = FFEpi<T, false>::eval(u.c, x, om2_of<V>(a));
         r.S = FFEpi<double, true>::eval(m, hi_of(x), a.prm.omega2);
     } else {
         if constexpr (std::is_same<V, dd>::value) {
@@ -123,6 +136,7 @@ __device__ __forceinline__ PtEval point_eval(const KernelArgs& a, const int32_t*
     }
     const double unit = std::is_same<V, dd>::value ? dd_unit() / kEps : 1.0;
     r.noise = residual_noise<PROB, T>(u.c, e, hi_of(x), kc, r.S, a.prm.omega2) * unit;
+    if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) r.noise += om2_err<V>(a) * r.S;
     r.res_re = re_hi(res);
     r.res_im = im_hi(res);
     r.res_abs = mag(res);
@@ -578,7 +592,7 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
         T res;
         double S;
         if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) {
-            res = FFEpi<T, false>::eval(u.c, x, a.prm.omega2);
+            res = FFEpi<T, false>::eval(u.c, x, om2_of<dd>(a));
             S = FFEpi<double, true>::eval(m, x.hi, a.prm.omega2);
         } else {
             dd kc[4];

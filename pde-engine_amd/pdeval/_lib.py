@@ -42,7 +42,8 @@ class Params(C.Structure):
                 ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32),
                 ('strict_symbolic', C.c_int32), ('reserved', C.c_int32),
                 ('noise_kappa', C.c_double), ('point_abs_tol', C.c_double),
-                ('res_rel_acc', C.c_double), ('omega2', C.c_double)]
+                ('res_rel_acc', C.c_double), ('omega2', C.c_double),
+                ('omega2_lo', C.c_double)]
 
 
 class Outputs(C.Structure):

@@ -679,11 +679,11 @@ class BatchValidator:
         self.kerr = kerr if kerr is not None or self.pd.problem_id != PROBLEM_KERR else default_kerr_constants()
         self.ctx = Context(self.pd.problem_id, device=device, kerr=kerr)
         self.params = params if params is not None else default_params(self.pd.problem_id)
-        # force-free, rotating field lines: Omega (a constant, as a string of an exact number
-        # whose square is a double: omega2_value) -> params.omega2 (validator.py:326-329)
+        # force-free, rotating field lines: Omega (a constant whose square is rational, as a
+        # string: omega2_value) -> params.omega2 + omega2_lo (validator.py:326-329)
         self.omega = omega
         if self.pd.problem_id == PROBLEM_FORCE_FREE:
-            self.params.omega2 = omega2_value(omega)
+            self.params.omega2, self.params.omega2_lo = omega2_value(omega)
         if symbolic not in SYMBOLIC_MODES:
             raise ValueError(f'symbolic mode {symbolic!r}: one of {SYMBOLIC_MODES}')
         self.symbolic = symbolic
@@ -776,18 +776,25 @@ _VALIDATORS: Dict[tuple, BatchValidator] = {}
 _VLOCK = threading.Lock()
 
 
-def omega2_value(omega) -> float:
-    """Omega**2 of the force-free rotating constraint as a double, exact (so the device's
-    Omega^2 is the reference's): Omega a constant whose square is a rational representable in
-    double precision (1, 2, 1/2, sqrt(2), ...).  A symbolic Omega (the reference allows a
-    function of u, validator.py:45) or an inexact square raises NotImplementedError."""
+def omega2_value(omega) -> Tuple[float, float]:
+    """Omega**2 of the force-free rotating constraint as a double-double (hi, lo), hi the
+    nearest double and lo = the rest rounded: Omega a constant whose square is rational (1, 2,
+    1/2, sqrt(2), 1/3, sqrt(2)/3, ...).  The grid stages take hi; the point stage's
+    double-double tier takes hi + lo, which carries a square that is no double (1/9) to 2^-106
+    relative, and its error bounds carry that representation error (pdeval_point.h om2_err).
+    A Float Omega is its exact binary value.  A symbolic Omega (the reference allows a function
+    of u, validator.py:45) or an irrational square raises NotImplementedError."""
     w = sp.sympify(omega)
     if w.free_symbols:
         raise NotImplementedError(f'Omega = {omega!r}: only a constant Omega is implemented')
-    w2 = sp.nsimplify(w ** 2, rational=True)
-    if not w2.is_Rational or sp.Rational(float(w2)) != w2:
-        raise NotImplementedError(f'Omega = {omega!r}: Omega**2 must be exact in double precision')
-    return float(w2)
+    if w.is_Float:
+        w = sp.Rational(w)
+    w2 = sp.simplify(sp.expand(w ** 2))
+    if not w2.is_Rational:
+        raise NotImplementedError(f'Omega = {omega!r}: Omega**2 must be rational')
+    hi = float(w2)
+    lo = float(w2 - sp.Rational(hi))
+    return hi, lo
 
 
 def get_validator(problem: str, device: int = 0, kerr=None, omega: str = '0') -> BatchValidator:

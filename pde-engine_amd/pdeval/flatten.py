@@ -530,10 +530,43 @@ def _det_kind(n):
     return None
 
 
+def _log_term(n) -> bool:
+    """A top-level additive term c * log(g) (c a rational constant, g of kind 'R' or 'P'): every
+    derivative of log(r * prod h_k**a_k) = log r + sum a_k log h_k is a rational function with
+    rational coefficients, so the term adds rational functions to u's derivatives.
+    (u = z + log(1 - rho**2/9) at Omega = 1/3: the reference's det at p* is a Number.)"""
+    while True:
+        if n[0] == 'neg':
+            n = n[1]
+        elif n[0] == 'mul' and (n[1][0] == 'm' or n[1][0] == 'c' and n[1][3]):
+            n = n[2]
+        elif n[0] in ('mul', 'div') and (n[2][0] == 'm' or n[2][0] == 'c' and n[2][3]):
+            n = n[1]
+        else:
+            break
+    if n[0] != 'log':
+        return False
+    kind = _det_kind(n[1])
+    return kind == 'R' or isinstance(kind, tuple)
+
+
+def _top_terms(n) -> list:
+    """The top-level additive terms of u (through add / sub / neg)."""
+    if n[0] in ('add', 'sub'):
+        return _top_terms(n[1]) + _top_terms(n[2])
+    if n[0] == 'neg':
+        return _top_terms(n[1])
+    return [n]
+
+
 def det_rational(ir) -> bool:
     """True when the force-free determinant of this program is rational at rational points.
     Top-level additive constants and rational constant factors do not matter (the
-    determinant sees only derivatives, and is homogeneous)."""
+    determinant sees only derivatives, and is homogeneous); nor do top-level log terms of
+    rational or power-product arguments (_log_term), beside other rational terms."""
+    terms = [t for t in _top_terms(ir) if not (t[0] in ('c', 'm') or _det_kind(t) == 'C')]
+    if any(_log_term(t) for t in terms) and all(_log_term(t) or _det_kind(t) == 'R' for t in terms):
+        return True
     n = ir
     while True:
         k = n[0]

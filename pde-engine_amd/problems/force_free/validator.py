@@ -38,7 +38,7 @@ class PreciseFoliationValidator:
                  device: int = 0, symbolic: Optional[str] = None, symbolic_timeout: float = 60.0):
         from pdeval.batch import SYMBOLIC_MODES, omega2_value
         if Omega != 0:
-            omega2_value(Omega)     # a constant whose square is exact, else NotImplementedError
+            omega2_value(Omega)     # a constant whose square is rational, else NotImplementedError
         self._omega_key = '0' if Omega == 0 else str(sp.nsimplify(sp.sympify(Omega)))
         self.symbolic = symbolic or os.environ.get('PDEVAL_SYMBOLIC', 'off')
         if self.symbolic not in SYMBOLIC_MODES:

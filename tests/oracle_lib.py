@@ -25,6 +25,7 @@ def load():
         _lib.oracle_jet.argtypes = [C.c_int, vp, C.c_int64, C.c_double, C.c_double, C.c_int, vp, vp]
         _lib.oracle_point.argtypes = [C.c_int, vp, C.c_int64, C.c_double, C.c_double, C.c_int, vp]
         _lib.oracle_set_omega2.argtypes = [C.c_double]
+        _lib.oracle_set_omega2_lo.argtypes = [C.c_double]
         _lib.oracle_set_kerr_constants.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int64,
                                                    C.c_double, C.c_double, C.c_int, C.c_int]
     return _lib
@@ -46,13 +47,15 @@ class _Params(C.Structure):
                 ('kerr_abs_tol', C.c_double), ('full_grid', C.c_int32), ('max_bad', C.c_int32),
                 ('strict_symbolic', C.c_int32), ('reserved', C.c_int32),
                 ('noise_kappa', C.c_double), ('point_abs_tol', C.c_double),
-                ('res_rel_acc', C.c_double), ('omega2', C.c_double)]
+                ('res_rel_acc', C.c_double), ('omega2', C.c_double),
+                ('omega2_lo', C.c_double)]
 
 
 def params(tau_point=1e-10, tau_grid=1e-7, kerr_abs_tol=1e-10, full_grid=1, max_bad=0,
-           strict_symbolic=1, noise_kappa=16.0, point_abs_tol=1e-20, res_rel_acc=1e-11, omega2=0.0):
+           strict_symbolic=1, noise_kappa=16.0, point_abs_tol=1e-20, res_rel_acc=1e-11, omega2=0.0,
+           omega2_lo=0.0):
     return _Params(tau_point, tau_grid, kerr_abs_tol, full_grid, max_bad, strict_symbolic, 0,
-                   noise_kappa, point_abs_tol, res_rel_acc, omega2)
+                   noise_kappa, point_abs_tol, res_rel_acc, omega2, omega2_lo)
 
 
 def validate(problem_id, ops, offsets, prm=None, first=0, count=-1, n_ref=None):
@@ -90,6 +93,7 @@ def set_omega2(w):
     """Force-free Omega^2 of the oracle's oracle_point / oracle_jet (oracle_validate takes it
     from its params)."""
     load().oracle_set_omega2(float(w))
+    load().oracle_set_omega2_lo(0.0)
 
 
 def point(problem_id, words, x, y, cplx=False):

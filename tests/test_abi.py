@@ -5,6 +5,7 @@ import re
 
 import numpy as np
 import pytest
+import sympy as sp
 
 from pdeval import _lib
 from pdeval import opcodes as OPC
@@ -41,12 +42,12 @@ def test_opcodes_match_header():
 
 def test_params_struct_layout():
     import ctypes as C
-    assert C.sizeof(_lib.Params) == 72
+    assert C.sizeof(_lib.Params) == 80
     assert C.sizeof(_lib.Outputs) == 64
     p = _lib.default_params(0)
     assert p.tau_point == 1e-10 and p.kerr_abs_tol == 1e-10 and p.full_grid == 1
     assert p.point_abs_tol == 1e-20 and p.res_rel_acc == 1e-11 and p.noise_kappa == 16.0
-    assert p.omega2 == 0.0
+    assert p.omega2 == 0.0 and p.omega2_lo == 0.0
     assert int(re.search(r'PDEVAL_N_PASSES\s+(\d+)', HEADER).group(1)) == _lib.N_PASSES
     assert int(re.search(r'PDEVAL_IMM_DD\s+\(1u << (\d+)\)', HEADER).group(1)) == OPC.IMM_DD.bit_length() - 1
 
@@ -79,13 +80,21 @@ def test_create_without_gpu_fails_loudly():
 
 
 def test_plugin_omega_contract():
-    """Omega != 0 (validator.py:326-329): a constant whose square is an exact double is taken
-    (params.omega2 on the device); a symbolic Omega -- the reference allows a function of u --
-    or an inexact square raises NotImplementedError before any GPU use."""
+    """Omega != 0 (validator.py:326-329): a constant whose square is rational is taken, as a
+    double-double (params.omega2, omega2_lo: 1/9 to 2^-106); a symbolic Omega -- the reference
+    allows a function of u -- or an irrational square raises NotImplementedError before any GPU
+    use."""
+    from fractions import Fraction
     from pdeval.batch import omega2_value
     from problems.force_free.validator import PreciseFoliationValidator
-    assert omega2_value(1) == 1.0 and omega2_value('1/2') == 0.25 and omega2_value('sqrt(2)') == 2.0
+    assert omega2_value(1) == (1.0, 0.0) and omega2_value('1/2') == (0.25, 0.0)
+    assert omega2_value('sqrt(2)') == (2.0, 0.0)
+    for w, exact in (('1/3', Fraction(1, 9)), ('sqrt(2)/3', Fraction(2, 9)), ('7/10', Fraction(49, 100))):
+        hi, lo = omega2_value(w)
+        assert lo != 0.0 and hi == float(exact) and abs(Fraction(hi) + Fraction(lo) - exact) <= exact * 2.0 ** -106
+    assert omega2_value(0.5) == (0.25, 0.0)     # a Float: its exact binary value
     assert PreciseFoliationValidator(Omega=1)._omega_key == '1'
-    for bad in ('1/3', 0.3, 'rho'):
+    assert PreciseFoliationValidator(Omega=sp.Rational(1, 3))._omega_key == '1/3'
+    for bad in ('2**(1/4)', 'pi', 'rho'):
         with pytest.raises(NotImplementedError):
             PreciseFoliationValidator(Omega=bad)

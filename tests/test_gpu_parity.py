@@ -532,3 +532,32 @@ def test_plugin_omega1_reference_verdicts():
     # exactly where the reference's do (Dipolar, Bent ... pass at Omega = 0)
     v0 = PreciseFoliationValidator()
     assert v0.validate(sp.sympify('rho**2*exp(-2*z)'), check_regularity=False)[0] is True
+
+
+def test_plugin_omega_third_reference_verdicts():
+    """Omega = 1/3 on the GPU: Omega^2 = 1/9 is no double, so params carry it as a double-double
+    (omega2 + omega2_lo) into the point stage's second tier.  The reference's verdict and text
+    on every decided row it ran with Omega = 1/3 (tests/golden/ref/ff_omega13_*.jsonl), among
+    them u = z + log(1 - rho**2/9), a solution only at Omega^2 = 1/9 exactly (accepted; with
+    Omega^2 rounded to a double the point stage rejects it, test_oracle_omega_third_*)."""
+    import os
+    from problems import load_problem
+    from problems.force_free.validator import PreciseFoliationValidator
+    import sympy as sp
+    files = [f for f in ('ff_omega13_known.jsonl', 'ff_omega13_d3_s300.jsonl')
+             if os.path.exists(os.path.join(G.GOLDEN, 'ref', f))]
+    rows = G.decided(G.ref_rows(*files))
+    prob = load_problem('force_free')
+    locs = {**prob.symbols, **prob.constants, **prob.unary_ops}
+    v = PreciseFoliationValidator(Omega=sp.Rational(1, 3))
+    assert v.validate(sp.sympify('z + log(1 - rho**2/9)', locals=locs), check_regularity=False) == \
+        (True, 'Valid foliation (Lean: det = 0 symbolically)')
+    got = v.validate_batch([sp.sympify(r['expr'], locals=locs) for r in rows], check_regularity=False,
+                           fast_point_only=False)
+    bad = [(r['expr'], r['reason'], g) for g, r in zip(got, rows) if g != (r['ok'], r['reason'])]
+    assert all(g[0] is False and 'expanded det' in rr for _, rr, g in bad) and len(bad) <= 2, bad[:5]
+    if bad:
+        vt = PreciseFoliationValidator(Omega=sp.Rational(1, 3), symbolic='text')
+        assert vt.validate_batch([sp.sympify(e, locals=locs) for e, _, _ in bad], check_regularity=False) == \
+            [(False, rr) for _, rr, _ in bad]
+    assert v.validate_strings([r['expr'] for r in rows]) == got

@@ -50,3 +50,31 @@ def test_keys_equal_the_reference_run_table():
         if got.degenerate or (got.normalized, got.signature) != (r['normalized'], r['signature']):
             bad.append((r['expression'], got, r['normalized'], r['signature']))
     assert not bad, bad[:3]
+
+
+def test_d4_stream_prefix_reaches_validate_as_in_reference():
+    """The force-free depth-4 stream (147,247 rows of the reference's enumerator, in stream
+    order; its first rows are the shallower candidates): the prefix's kept rows equal the
+    reference's own filters' (streams/force_free_d4_validated.txt.gz, 142,004 rows)."""
+    n = 250
+    with gzip.open(os.path.join(G.GOLDEN, 'streams', 'force_free_d4.txt.gz'), 'rt') as f:
+        rows = [l.rstrip('\n').split('\t') for _, l in zip(range(n), f)]
+    with gzip.open(os.path.join(G.GOLDEN, 'streams', 'force_free_d4_validated.txt.gz'), 'rt') as f:
+        ref = [int(l.split('\t')[0]) for l in f]
+    res = F.filter_stream('force_free', [r[-1] for r in rows])
+    assert res.kept == [i for i in ref if i < n]
+
+
+def test_d4_full_run_record():
+    """The whole depth-4 stream through pdeval.prefilter over the SymPy pool
+    (scripts/prefilter_d4.py, run in the build container; its record is committed): the kept
+    rows equal the reference's, and the record carries the wall time and pool size the
+    end-to-end figure uses."""
+    import glob
+    recs = sorted(glob.glob(os.path.join(os.path.dirname(G.GOLDEN), '..', 'profiles', '*_prefilter_d4.json')))
+    assert recs, 'no committed prefilter_d4 record (scripts/prefilter_d4.py)'
+    with open(recs[-1]) as f:
+        rec = json.load(f)
+    assert rec['rows'] == 147247 and rec['kept'] == 142004 == rec['reference_kept']
+    assert rec['kept_equals_reference'] is True, (rec['only_here'][:5], rec['only_reference'][:5])
+    assert rec['wall_s'] > 0 and rec['procs'] >= 1
