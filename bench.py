@@ -313,6 +313,11 @@ class ProblemBench:
                                       shuffle=not os.environ.get('PD_BENCH_STREAM_ORDER'))
         # algorithmic work of the batch; it also balances the shards
         self.flops_prog = WL.flops_per_program(pid, self.ops_all, self.off_all)
+        # the part the lean passes evaluate once per grid row (hoisted x-only prefixes, DESIGN.md
+        # §3), unless the library runs with PDEVAL_HOIST=0
+        self.hoist = os.environ.get('PDEVAL_HOIST', '1') != '0'
+        self.flops_hoist = WL.flops_per_program(pid, self.ops_all, self.off_all, hoisted=True) \
+            if self.hoist else np.zeros_like(self.flops_prog)
         plan = WL.rank_plan(self.tiled, world, rank, self.flops_prog)
         self.ranges, self.idx, self.n = plan.ranges, plan.idx, plan.n
         self.ops, self.off = WL.gather_programs(self.ops_all, self.off_all, self.idx)
@@ -419,11 +424,15 @@ class ProblemBench:
         depth = (hdr >> 8) & 0xff
         cflag = (hdr & FLAG_COMPLEX) != 0
         in_p1 = (depth <= 2) & ~cflag
-        fl = self.flops_prog[self.idx]
+        # per candidate: its program's flops at every point, less the hoisted prefix, which runs
+        # once per grid row (64 rows of the default grid)
+        rows = 64
+        fh = self.flops_hoist[self.idx]
+        fl = (self.flops_prog[self.idx] - fh) * self.npts + fh * rows
         # candidates pass 1 re-routed to the complex pass after the point stage: their grid work
         # is not pass 1's (charged at the pass-1 mean, a conservative correction)
         rerouted = max(0, counts['complex'] - int(cflag.sum())) if self.pid == PROBLEM_FORCE_FREE else 0
-        p1_flops = (float(fl[in_p1].sum()) - rerouted * float(fl[in_p1].mean() if in_p1.any() else 0.0)) * self.npts
+        p1_flops = float(fl[in_p1].sum()) - rerouted * float(fl[in_p1].mean() if in_p1.any() else 0.0)
         p1_ms = pass_ms['pass1_stack2']
         achieved_tf = p1_flops / (p1_ms * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic(int(in_p1.sum()), self.dominant)
@@ -431,7 +440,8 @@ class ProblemBench:
                 'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS,
                 'traffic': traffic, 'traffic_source': traffic_src,
                 'kernel_ms': p1_ms, 'kernel_candidates': int(in_p1.sum()) - rerouted,
-                'flops_per_launch': p1_flops}
+                'flops_per_launch': p1_flops,
+                'flops_model': 'hoisted prefixes once per row' if self.hoist else 'every opcode at every point'}
         roof.update(pmc_flop_frac(self.dominant, int(in_p1.sum()) - rerouted, p1_ms))
         return {'roofline': roof, 'pass_ms': {k: round(v, 3) for k, v in pass_ms.items()}, 'counts': counts}
 

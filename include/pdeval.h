@@ -293,6 +293,10 @@ int pdeval_program_depth(const int32_t* ops, int64_t n_words);
 
 /* Algorithmic cost model: FP64 flops per grid point for one program.      */
 double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words);
+/* The part of it the lean grid passes evaluate 64 times per candidate (once per grid row or
+ * lane), not per point: the program's hoisted prefix of one coordinate (DESIGN.md §3
+ * "Hoisted prefixes"); 0 if none.                                                      */
+double pdeval_program_hoist_flops(int problem_id, const int32_t* ops, int64_t n_words);
 
 const char* pdeval_version(void);
 

@@ -113,6 +113,10 @@ struct pdeval_ctx {
     uint8_t* d_pstate = nullptr;    // point-stage state, capacity cap
     int32_t* d_dec = nullptr;       // decoded programs of the lean grid passes, dec_cap words
     int64_t dec_cap = 0;
+    // the hoisted x-only prefixes of the lean passes (pdeval_grid.h PD_HOIST): cap x (K + 1) x 64
+    // doubles (env PDEVAL_HOIST=0: none, A/B)
+    bool hoist = true;
+    double* d_hoist = nullptr;
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
     double* d_noise = nullptr;      // fp64 noise bounds at the reference points, cap * 4
     T2Acc* d_t2acc = nullptr;       // tier-2 accumulators, cap entries, zero between launches
@@ -431,6 +435,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_DD_EARLY")) c->dd_early = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_LIST_QUEUE")) c->list_queue = std::max(0, atoi(v));
     if (const char* v = getenv("PDEVAL_LIST_PARTS")) c->list_parts = std::min(16, std::max(1, atoi(v)));
+    if (const char* v = getenv("PDEVAL_HOIST")) c->hoist = atoi(v) != 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     if ((e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess)
@@ -466,6 +471,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->d_pstate) (void)hipFree(c->d_pstate);
     if (c->d_ddps) (void)hipFree(c->d_ddps);
     if (c->d_dec) (void)hipFree(c->d_dec);
+    if (c->d_hoist) (void)hipFree(c->d_hoist);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
     if (c->d_t2acc) (void)hipFree(c->d_t2acc);
@@ -571,8 +577,8 @@ extern "C" int pdeval_program_depth(const int32_t* ops, int64_t n_words) {
 // and the mixed one feeds nothing else, so it is not counted (nor computed by the lean passes).
 // Products: coefficient (i, j) of a jet product takes (i+1)(j+1) of them, so a full product is
 // 70 for K = 4 (2*70 - 15 = 125 flops) and 11 for Kerr's 5 coefficients (2*11 - 5 = 17).
-extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words) {
-    const bool ff = problem_id == PDEVAL_PROBLEM_FORCE_FREE;
+// FP64 flops of one opcode at one sample point (the model of pdeval_program_flops)
+static double op_flops(bool ff, uint32_t w) {
     const int K = ff ? 4 : 2;
     const double NC = ff ? 15.0 : 5.0;
     const double mulf = ff ? 125.0 : 17.0;
@@ -580,36 +586,102 @@ extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64
     // Horner composition: sum over levels (2*#products) + coefficient chain (Kerr: the level
     // products of h (h_00 = 0) into the 5 coefficients, 6 + 2)
     const double compf = ff ? (2.0 * 91.0 + 3.0 * K) : (2.0 * 8.0 + 3.0 * K);
+    switch (w & 0xffu) {
+        case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: return NC;
+        case PDOP_MUL: return mulf;
+        case PDOP_DIV: case PDOP_RDIV: case PDOP_RDIVC: return divf;
+        case PDOP_ADDC: case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: return 2;
+        case PDOP_MULC: case PDOP_NEG: case PDOP_ABS: return NC;
+        case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: return 2 * NC;
+        case PDOP_POWN: {
+            int n = (w >> 8) & 0xff, m = 0;
+            while (n > 1) { m += 1 + (n & 1); n >>= 1; }
+            return m * mulf;
+        }
+        case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: return compf;
+        // coordinate powers: K+1 coefficients, then a sparse (univariate) product/quotient
+        case PDOP_PUSH_P: return 3 * (K + 1);
+        case PDOP_ADD_P: case PDOP_SUB_P: return 4 * (K + 1);
+        case PDOP_MUL_P: return 3 * (K + 1) + (ff ? 50.0 : 11.0);
+        case PDOP_DIV_P: return 3 * (K + 1) + (ff ? 60.0 : 15.0);
+        case PDOP_RDIV_P: return 3 * (K + 1) + divf;
+        default: return 0.0;
+    }
+}
+
+extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words) {
+    const bool ff = problem_id == PDEVAL_PROBLEM_FORCE_FREE;
     double f = 0.0;
     for (int64_t pc = 1; pc < n_words;) {
-        const uint32_t op = (uint32_t)ops[pc] & 0xffu;
-        switch (op) {
-            case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: f += NC; break;
-            case PDOP_MUL: f += mulf; break;
-            case PDOP_DIV: case PDOP_RDIV: case PDOP_RDIVC: f += divf; break;
-            case PDOP_ADDC: case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: f += 2; break;
-            case PDOP_MULC: case PDOP_NEG: case PDOP_ABS: f += NC; break;
-            case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: f += 2 * NC; break;
-            case PDOP_POWN: {
-                int n = (ops[pc] >> 8) & 0xff, m = 0;
-                while (n > 1) { m += 1 + (n & 1); n >>= 1; }
-                f += m * mulf;
-                break;
-            }
-            case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: f += compf; break;
-            // coordinate powers: K+1 coefficients, then a sparse (univariate) product/quotient
-            case PDOP_PUSH_P: f += 3 * (K + 1); break;
-            case PDOP_ADD_P: case PDOP_SUB_P: f += 4 * (K + 1); break;
-            case PDOP_MUL_P: f += 3 * (K + 1) + (ff ? 50.0 : 11.0); break;
-            case PDOP_DIV_P: f += 3 * (K + 1) + (ff ? 60.0 : 15.0); break;
-            case PDOP_RDIV_P: f += 3 * (K + 1) + divf; break;
-            default: break;
-        }
+        f += op_flops(ff, (uint32_t)ops[pc]);
         pc += op_words(ops[pc]);
     }
     // epilogue: force-free determinant + its magnitude shadow; Kerr 4-term operator + scale
     f += ff ? 2.0 * 160.0 : 16.0;
     return f;
+}
+
+// The part of pdeval_program_flops that the lean passes evaluate once per grid row (x alone)
+// or once per lane (y alone) instead of once per point: the program's hoisted prefix as
+// pdeval_grid.h decode_kernel finds it (the longest prefix ending at stack depth 1 whose value
+// depends on one coordinate only, holding a heavy opcode, not the whole program; Kerr: PUSH_C +
+// MUL_X / MUL_Y / MUL_P decode into one push).
+extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops, int64_t n_words) {
+    const bool ff = problem_id == PDEVAL_PROBLEM_FORCE_FREE;
+    if (pdeval_program_depth(ops, n_words) < 1) return 0.0;
+    uint32_t msk[PDEVAL_MAX_STACK + 2] = {};
+    int d = 0;
+    double f = 0.0, f_at = 0.0;
+    bool heavy = false, heavy_at = false;
+    int64_t at = -1;
+    for (int64_t pc = 1; pc < n_words;) {
+        const uint32_t w = (uint32_t)ops[pc];
+        const uint32_t op = w & 0xffu;
+        int64_t len = op_words(ops[pc]);
+        const bool on_y = (w >> 16) & 1u;
+        if (!ff && op == PDOP_PUSH_C && pc + len < n_words) {   // (PD_FUSE_PUSHC = 1)
+            const uint32_t w2 = (uint32_t)ops[pc + len], op2 = w2 & 0xffu;
+            if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || op2 == PDOP_MUL_P) {
+                ++d;
+                msk[d] = (op2 == PDOP_MUL_Y || (op2 == PDOP_MUL_P && ((w2 >> 16) & 1u))) ? 2u : 1u;
+                f += op_flops(ff, w) + op_flops(ff, w2);
+                pc += len + 1;
+                if (d == 1) {
+                    if ((msk[1] & 4u) || msk[1] == 3u) break;
+                    at = pc; f_at = f; heavy_at = heavy;
+                }
+                continue;
+            }
+        }
+        switch (op) {
+            case PDOP_PUSH_X: msk[++d] = 1u; break;
+            case PDOP_PUSH_Y: msk[++d] = 2u; break;
+            case PDOP_PUSH_C: msk[++d] = 0u; break;
+            case PDOP_PUSH_I: msk[++d] = 4u; break;
+            case PDOP_PUSH_P: msk[++d] = on_y ? 2u : 1u; break;
+            case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: case PDOP_MUL: case PDOP_DIV: case PDOP_RDIV:
+                --d;
+                msk[d] |= msk[d + 1];
+                break;
+            case PDOP_ADD_X: case PDOP_SUB_X: case PDOP_MUL_X: case PDOP_DIV_X: msk[d] |= 1u; break;
+            case PDOP_ADD_Y: case PDOP_SUB_Y: case PDOP_MUL_Y: case PDOP_DIV_Y: msk[d] |= 2u; break;
+            case PDOP_ADD_P: case PDOP_SUB_P: case PDOP_MUL_P: case PDOP_DIV_P: case PDOP_RDIV_P:
+                msk[d] |= on_y ? 2u : 1u;
+                break;
+            default: break;
+        }
+        f += op_flops(ff, w);
+        heavy = heavy || op == PDOP_MUL || op == PDOP_DIV || op == PDOP_RDIV || op == PDOP_RDIVC ||
+                op == PDOP_POWN || op == PDOP_POW || op == PDOP_SQRT || op == PDOP_EXP || op == PDOP_LOG ||
+                op == PDOP_MUL_P || op == PDOP_DIV_P || op == PDOP_RDIV_P || op == PDOP_DIV_X;
+        pc += len;
+        if (d == 1) {
+            if ((msk[1] & 4u) || msk[1] == 3u) break;
+            at = pc; f_at = f; heavy_at = heavy;
+        }
+    }
+    // (a NEG the decoder folds away is charged like any opcode: the model folds none)
+    return (at > 0 && at < n_words && at < (1 << 14) && heavy_at) ? f_at : 0.0;
 }
 
 // ---------------------------------------------------------------------------- launches
@@ -656,6 +728,12 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (c->d_ddps) (void)hipFree(c->d_ddps);
     c->d_ddps = nullptr;
     HIPCHK(c, hipMalloc(&c->d_ddps, cap));
+    if (c->d_hoist) (void)hipFree(c->d_hoist);
+    c->d_hoist = nullptr;
+    if (c->hoist) {
+        const int K = c->problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
+        HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)cap * (K + 1) * 64 * sizeof(double)));
+    }
     if (c->d_status) (void)hipFree(c->d_status);
     c->d_status = nullptr;
     HIPCHK(c, hipMalloc(&c->d_status, cap));
@@ -814,6 +892,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.noise_ref = c->d_noise;
     a.t2acc = c->d_t2acc;
     a.dec = c->d_dec;
+    a.hoist = c->nx <= 64 ? c->d_hoist : nullptr;   // (one grid row per lane)
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
     // complex-valued ones -> L_CPLX.  Lanes take the candidates sorted by opcode sequence

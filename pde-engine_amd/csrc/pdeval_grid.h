@@ -125,6 +125,33 @@ __device__ __forceinline__ bool neg_fold_ok(const int32_t* prog, int plen) {
     return true;
 }
 
+// ---- x-only prefixes (PD_HOIST).  A program whose first opcodes compute a value of x alone
+// (u = exp(rho) * z: PUSH_X EXP | PUSH_Y MUL) computes the same jet at every lane of a grid row:
+// the lean passes evaluate that prefix once per candidate for all rows at once (one row per
+// lane), keep the jets in a per-candidate buffer and start every row's run after it.  A prefix
+// of y alone (u = sqrt(z + 1) * rho) is the same at every row: evaluated once at the lanes'
+// ordinates.  The decoder records the longest prefix of one coordinate ending at stack depth 1
+// in bits 17-30 of the header word (the position of the first opcode after it; 0 = none) and
+// bit 31 (1: a prefix of y), when it holds a heavy opcode.
+#ifndef PD_HOIST
+#define PD_HOIST 1
+#endif
+constexpr uint64_t kHeavyMask = op_bit(PDOP_MUL) | op_bit(PDOP_DIV) | op_bit(PDOP_RDIV) | op_bit(PDOP_RDIVC) |
+                                op_bit(PDOP_POWN) | op_bit(PDOP_POW) | op_bit(PDOP_SQRT) | op_bit(PDOP_EXP) |
+                                op_bit(PDOP_LOG) | op_bit(PDOP_MUL_P) | op_bit(PDOP_DIV_P) | op_bit(PDOP_RDIV_P) |
+                                op_bit(PDOP_DIV_X);
+__device__ __forceinline__ void hoist_track(int d, const uint32_t (&msk)[5], int pc, bool heavy, bool& alive,
+                                            int& hoist_last, bool& hoist_heavy, bool& hoist_y) {
+    if (!alive || d != 1) return;
+    if ((msk[1] & 4u) || msk[1] == 3u) {   // both coordinates, or the imaginary unit
+        alive = false;
+        return;
+    }
+    hoist_last = pc;
+    hoist_heavy = heavy;
+    hoist_y = msk[1] == 2u;
+}
+
 template <int PROB>
 __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     const int64_t cand = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -138,6 +165,12 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     bool ok = plen >= 2 && (hdr & 0xffu) == 0u;   // (COMPLEX programs: the lean complex pass)
     int pc = 1, d = 0, dmax = 0, last = -1;
     int sg[5] = {1, 1, 1, 1, 1};   // PD_FOLD_NEG: sign of the value at each stack depth (1-based)
+    // PD_HOIST: which coordinates the value at each stack depth depends on (bit 0 x, bit 1 y,
+    // bit 2 the imaginary unit), and the longest x-only prefix of the program that ends at
+    // depth 1 (its last visited opcode, and whether it holds a heavy opcode)
+    uint32_t msk[5] = {0u, 0u, 0u, 0u, 0u};
+    int hoist_last = -1;
+    bool hoist_alive = true, heavy = false, hoist_heavy = false, hoist_y = false;
     const bool fold = PD_FOLD_NEG && ok && neg_fold_ok(prog, plen);
     while (ok && pc < plen) {
         const uint32_t w = (uint32_t)prog[pc];
@@ -187,6 +220,8 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
                 dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << 21) |
                                     (1u << (24 + DG_PUSH)));
                 sg[d] = 1;
+                msk[d] = (op2 == PDOP_MUL_Y || (op2 == PDOP_MUL_P && ((w2 >> 16) & 1u))) ? 2u : 1u;
+                hoist_track(d, msk, pc, heavy, hoist_alive, hoist_last, hoist_heavy, hoist_y);
                 last = pc;
                 pc += len + 1;
                 continue;
@@ -259,12 +294,35 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
         }
         dec[pc] = (int32_t)(dop | (w & 0x1ff00u & ((kImmMask & b) ? 0u : ~0u)) | (dec_group(op_bit((int)dop)) << 17) |
                             ((uint32_t)len << 21) | (1u << (24 + dec_group(op_bit((int)dop)))));
+        // (masks follow the original opcode: a folded sign does not change what it depends on)
+        if ((kPushMask | op_bit(PDOP_PUSH_I)) & b) {
+            msk[d] = op == PDOP_PUSH_X ? 1u : op == PDOP_PUSH_Y ? 2u : op == PDOP_PUSH_I ? 4u
+                   : op == PDOP_PUSH_P ? (((w >> 16) & 1u) ? 2u : 1u) : 0u;
+        } else if (kBinMask & b) {
+            msk[d] |= msk[d + 1];
+        } else if ((kPOpMask & b) || op == PDOP_ADD_X || op == PDOP_SUB_X || op == PDOP_MUL_X ||
+                   op == PDOP_DIV_X || op == PDOP_ADD_Y || op == PDOP_SUB_Y || op == PDOP_MUL_Y ||
+                   op == PDOP_DIV_Y) {
+            const bool on_y = (kPOpMask & b) ? ((w >> 16) & 1u) != 0u
+                                             : (op == PDOP_ADD_Y || op == PDOP_SUB_Y || op == PDOP_MUL_Y || op == PDOP_DIV_Y);
+            msk[d] |= on_y ? 2u : 1u;
+        }
+        heavy = heavy || (kHeavyMask & b);
+        hoist_track(d, msk, pc, heavy, hoist_alive, hoist_last, hoist_heavy, hoist_y);
         last = pc;
         pc += len;
     }
     ok = ok && d == 1 && last >= 0;
     if (ok) dec[last] |= (int32_t)(1u << 20);
-    dec[0] = ok ? (int32_t)(((uint32_t)dmax << 8) | (sg[1] < 0 ? 1u << 16 : 0u)) : (int32_t)0xff;
+    // the hoisted prefix: the position of the first opcode after it (its last opcode's distance
+    // is final now -- a folded NEG after it extends that distance), or 0 for none
+    uint32_t hp = 0u;
+    if (PD_HOIST && ok && hoist_last >= 0 && hoist_heavy) {
+        const uint32_t at = (uint32_t)hoist_last + (((uint32_t)dec[hoist_last] >> 21) & 7u);
+        if (at < (uint32_t)plen && at < (1u << 14)) hp = at;   // (not a whole program of x alone)
+    }
+    dec[0] = ok ? (int32_t)(((uint32_t)dmax << 8) | (sg[1] < 0 ? 1u << 16 : 0u) | (hp << 17) |
+                            (hp && hoist_y ? 1u << 31 : 0u)) : (int32_t)0xff;
 }
 
 // ---- coordinate-power tables.  A coordinate power v**n (PDOP_*_P) enters the interpreter as
@@ -404,11 +462,13 @@ template <class T, int K, int W, int MAXD> struct Lean {
     // (one grid row each), y is the lane's ordinate.
     // coordinate-power coefficients of v**n at row slot q (x) or at the lane's ordinate (y)
     static constexpr int PTAB = K == 4 ? PD_PTAB : PD_PTAB_KERR;
+    // XL: x differs per lane (the hoisted prefix, one grid row per lane): vector loads
+    template <bool XL = false>
     static __device__ __forceinline__ void pco_x(const PowTab<W>& pt, const double (&x)[W], int q, int n, double* pk) {
         if constexpr (PTAB != 0) {
             const double* p = pt.px[q] + (size_t)n * pt.sx;
 #pragma unroll
-            for (int k = 0; k <= K; ++k) pk[k] = rd_sf64(p + k);
+            for (int k = 0; k <= K; ++k) pk[k] = XL ? p[k] : rd_sf64(p + k);
         } else {
             O::pcoefs(x[q], n, pk);
         }
@@ -423,21 +483,26 @@ template <class T, int K, int W, int MAXD> struct Lean {
         }
     }
 
+    // pc0: the first opcode to run -- 1, or the position after a hoisted prefix (PD_HOIST), with
+    // acc holding the prefix's value at stack depth 1.  PRE (XL: x per lane): stop before the
+    // opcode at `stop` (the hoisted prefix alone).
+    template <bool XL = false, bool PRE = false>
     static __device__ __forceinline__ void run(const int32_t* dec, const double (&x)[W], double y,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
-                                               T* stk, int lane, const PowTab<W>& pt) {
+                                               T* stk, int lane, const PowTab<W>& pt, int pc0 = 1,
+                                               int stop = 0) {
         // MAXD = 3 (pass 2): the upper of the two operand slots lives in VGPRs, the lower in
         // LDS -- two LDS slots of W = 2 Kerr jets (12 KiB per wave) held pass 2 at ~3 waves
         // per SIMD; with one, VGPRs set the occupancy
         J reg[RSLOT ? W : 1];
-        int pc = 1;
+        int pc = pc0;
         // an opcode word and the two after it (its f64 immediate, when it has one) are read
         // together, one op ahead, so an op's immediate is in SGPRs when its turn comes instead
         // of costing a dependent scalar load (dec[] is padded by 4 words past its end)
-        uint32_t w = rd_word(dec + 1);
-        double imm = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + 2) : 0.0;
-        bool first = true;
-        int d = 0;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
+        uint32_t w = rd_word(dec + pc0);
+        double imm = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + pc0 + 1) : 0.0;
+        bool first = pc0 == 1;
+        int d = pc0 == 1 ? 0 : 1;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
         for (;;) {
             const uint32_t op = w & 0xffu;
             const uint32_t grp = (w >> 17) & 7u;
@@ -488,7 +553,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                     } else {
 #pragma unroll
                         for (int q = 0; q < W; ++q) {
-                            pco_x(pt, x, q, pn, pk);
+                            pco_x<XL>(pt, x, q, pn, pk);
                             O::template set_p<0>(acc[q], pk);
                         }
                     }
@@ -519,7 +584,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
 #pragma unroll
                             for (int k = 1; k <= K; ++k) acc[q].c[ji(0, k)] = c * cvt<T>(pk[k]);
                         } else {
-                            pco_x(pt, x, q, pn, pk);
+                            pco_x<XL>(pt, x, q, pn, pk);
                             O::set_const(acc[q], c * cvt<T>(pk[0]));
 #pragma unroll
                             for (int k = 1; k <= K; ++k) acc[q].c[ji(k, 0)] = c * cvt<T>(pk[k]);
@@ -581,7 +646,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
                 } else {
 #pragma unroll
                     for (int q = 0; q < W; ++q) {
-                        pco_x(pt, x, q, pn, pk);
+                        pco_x<XL>(pt, x, q, pn, pk);
                         O::template p_op<0>(op, acc[q], pk);
                     }
                 }
@@ -631,7 +696,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
 #pragma unroll
                 for (int q = 0; q < W; ++q) acc[q].c[MIX] = zero<T>();
             }
-            if (!more) break;
+            if (!more || (PRE && npc == stop)) break;
             first = false;
             pc = npc;
             w = wn;
@@ -763,6 +828,48 @@ template <int PROB, int MAXD, class T = double> constexpr size_t grid_lds(int wa
     return (size_t)waves * L::LDS_SLOTS * L::SLOT * sizeof(T);
 }
 
+// The hoisted prefix (PD_HOIST) of one candidate.  x alone: lane r = grid row r, its pure-x
+// coefficients into hb[k][row]; y alone: lane j at its own ordinate (the prefix reads no x),
+// the pure-y coefficients into hb[k][j].  Returns `hoist`, or 0 when some lane carries a
+// non-zero coefficient outside those (a non-finite value: the row loop then runs the whole
+// program).  (PD_HOIST_NOINLINE=1, out of line: the call frame took 608 B of scratch)
+#ifndef PD_HOIST_NOINLINE
+#define PD_HOIST_NOINLINE 0
+#endif
+template <int K, int MAXD>
+#if PD_HOIST_NOINLINE
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+int hoist_prefix(const int32_t* dec, int hoist, bool hy, const double* gx, int nx, int ny, const double* ptab,
+                 double* hb, int lane, double* stk, double y0, double inv_y0) {
+    using L1 = Lean<double, K, 1, MAXD>;
+    const int r = min(lane, nx - 1);
+    const double xl[1] = {gx[r]}, ixl[1] = {gx[nx + r]};
+    PowTab<1> p1;
+    p1.sx = nx * (K + 1);
+    p1.sy = (K + 1) * ny;
+    p1.ny = ny;
+    p1.px[0] = ptab + (size_t)r * (K + 1);
+    p1.py = ptab + (size_t)PTAB_N * nx * (K + 1) + lane;
+    typename L1::J h[1];
+    L1::template run<true, true>(dec, xl, y0, ixl, inv_y0, h, stk, lane, p1, 1, hoist);
+    bool dirty = false;
+#pragma unroll
+    for (int c = 0; c < nc(K); ++c) {
+        bool pure = false;
+#pragma unroll
+        for (int k = 0; k <= K; ++k) pure = pure || c == (hy ? ji(0, k) : ji(k, 0));
+        if (!pure) dirty = dirty || !(h[0].c[c] == 0.0);
+    }
+    if (__any(dirty)) return 0;
+#pragma unroll
+    for (int k = 0; k <= K; ++k) hb[k * 64 + lane] = h[0].c[hy ? ji(0, k) : ji(k, 0)];
+    __threadfence_block();   // the rows read other lanes' values
+    return hoist;
+}
+
 // The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots, jets
 // over T: double, or cplx for the force-free candidates not real at p* (the complex pass, whose
 // point stage point_list_kernel<.., cplx> decided).
@@ -800,10 +907,17 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     // the decoded program (decode_kernel, run before pass 1): 0xff = not for the lean passes;
     // its true stack depth must fit this pass's slots
     uint32_t u_sgn = 0u;   // a sign the decoder folded out of the program (PD_FOLD_NEG), bit 31
+    int hoist = 0;         // PD_HOIST: the first opcode after the program's hoisted prefix, or 0
+    bool hy = false;       // ... a prefix of y alone
     if (!slow) {
         const uint32_t dh = rd_word(a.dec + beg);
         slow = (dh & 0xffu) != 0u || (int)((dh >> 8) & 0xffu) > MAXD;
         u_sgn = (dh & 0x10000u) << 15;
+        if (!CX && PD_HOIST && a.hoist && parts == 1) {
+            hoist = (int)((dh >> 17) & 0x3fffu);
+            hy = (dh >> 31) != 0u;
+            if (hy && a.ny != 64) hoist = 0;   // (one ordinate per lane)
+        }
     }
     if (slow) {
         if (lane == 0 && part == 0) list_append(slow_list, slow_count, a.list_capacity, cand);
@@ -816,6 +930,20 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     // rcp(per_row == 1 ? y0 : y) and the IEEE reciprocal (11 VALU) runs once per row instead of
     // once per candidate
     if constexpr (PD_INVY_PIN) pin_f64(inv_y0);
+    // the prefix of one coordinate (PD_HOIST), once for every row: x alone, lane r evaluates it
+    // at x = gx[r]; y alone, each lane at its own ordinate -- the same opcodes on the same values
+    // as the row loop would, so the same jets -- and its pure-x (pure-y) coefficients go to the
+    // candidate's slot of a.hoist; every row then starts its run after the prefix with those
+    // coefficients and the others 0.  The others are exact zeros of either sign (products with
+    // the 0 coefficients of the coordinate's jet), and no jet operation divides by a coefficient
+    // other than the value, so a zero's sign changes no result; where a lane carries a
+    // non-finite coefficient (0 * inf = NaN in the others) the candidate is not hoisted.
+    // (a.nx <= 64, checked by the host, which passes a.hoist = NULL otherwise)
+    if constexpr (!CX && PD_HOIST) {
+        if (hoist)
+            hoist = hoist_prefix<K, MAXD>(a.dec + beg, hoist, hy, a.gx, a.nx, a.ny, a.ptab,
+                                          a.hoist + (size_t)cand * (K + 1) * 64, lane, stk, y0, inv_y0);
+    }
     GridMax<PROB != PDEVAL_PROBLEM_FORCE_FREE> gm;   // (PD_DIVFREE) the lane's running maximum of q
     double qmax = 0.0;
     int nbad = 0, nfin = 0;
@@ -873,7 +1001,22 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             constexpr bool kv_late = W > 2 || (MAXD == 2 && PD_KV_LATE) || (MAXD > 2 && PD_KV_LATE_DEEP);
             if constexpr (!kv_late) load_kv();
             J u[W];
-            L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane, pt);
+            if (!CX && PD_HOIST && hoist) {
+                const double* hb = a.hoist + (size_t)cand * (K + 1) * 64;
+#pragma unroll
+                for (int q = 0; q < W; ++q) {
+#pragma unroll
+                    for (int c = 0; c < nc(K); ++c) u[q].c[c] = zero<T>();
+                    if (hy) {
+#pragma unroll
+                        for (int k = 0; k <= K; ++k) u[q].c[ji(0, k)] = cvt<T>(hb[k * 64 + lane]);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k <= K; ++k) u[q].c[ji(k, 0)] = cvt<T>(hb[k * 64 + min(row + q, a.nx - 1)]);
+                    }
+                }
+            }
+            L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane, pt, hoist ? hoist : 1);
             if constexpr (kv_late) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {

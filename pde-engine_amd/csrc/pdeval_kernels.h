@@ -79,6 +79,9 @@ struct KernelArgs {
     struct T2Acc* t2acc;        // tier 2: one accumulator per list entry (pdeval_tier2.h), zeroed
     const int32_t* perm;        // order of pass 0 and the tier-B collect pass (pdeval_sort.hip), or NULL
     int32_t* dec;               // n_words: the programs pre-decoded for the lean grid passes
+    double* hoist;              // lean passes: per candidate, the pure-x coefficients of its
+                                // x-only prefix at every grid row, [cand][k][row] (pdeval_grid.h
+                                // PD_HOIST); NULL = not hoisted
                                 // (pdeval_grid.h decode_kernel), or NULL
     // the problem's constants per stage (PDEVAL_IMM_PRM; Kerr M, a): point stage (fp64 and
     // double-double) and the constant test / grid stage

@@ -21,7 +21,8 @@ LIB_PATH = os.environ.get('PDEVAL_LIB', os.path.join(_HERE, '..', 'lib', 'libpde
 EXPORTS = (
     'pdeval_create', 'pdeval_destroy', 'pdeval_last_error', 'pdeval_n_ref_points',
     'pdeval_n_points', 'pdeval_default_params', 'pdeval_validate_batch',
-    'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_version',
+    'pdeval_validate_device', 'pdeval_program_depth', 'pdeval_program_flops', 'pdeval_program_hoist_flops',
+    'pdeval_version',
     'pdeval_set_timing', 'pdeval_pass_times', 'pdeval_pass_counts', 'pdeval_eval_points',
     'pdeval_compile_batch', 'pdeval_canonical', 'pdeval_point_eval', 'pdeval_point_states',
     'pdeval_comm_unique_id', 'pdeval_comm_init', 'pdeval_gather_bits', 'pdeval_comm_destroy',
@@ -93,6 +94,8 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_program_depth.argtypes = [vp, i64]
     lib.pdeval_program_flops.argtypes = [C.c_int, vp, i64]
     lib.pdeval_program_flops.restype = dbl
+    lib.pdeval_program_hoist_flops.argtypes = [C.c_int, vp, i64]
+    lib.pdeval_program_hoist_flops.restype = dbl
     lib.pdeval_version.restype = C.c_char_p
     lib.pdeval_set_timing.argtypes = [vp, C.c_int]
     lib.pdeval_pass_times.argtypes = [vp, vp, C.c_int, vp]

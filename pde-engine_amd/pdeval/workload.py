@@ -59,14 +59,16 @@ def gather_programs(ops: np.ndarray, offsets: np.ndarray, idx: np.ndarray):
     return ops[starts], new_off
 
 
-def flops_per_program(problem_id: int, ops: np.ndarray, offsets: np.ndarray) -> np.ndarray:
-    """pdeval_program_flops of every program of a table (FP64 flops per sample point)."""
+def flops_per_program(problem_id: int, ops: np.ndarray, offsets: np.ndarray, hoisted: bool = False) -> np.ndarray:
+    """pdeval_program_flops of every program of a table (FP64 flops per sample point), or with
+    hoisted=True pdeval_program_hoist_flops: the part of it the lean passes evaluate once per
+    grid row (the hoisted x-only prefix)."""
     from ._lib import load
     lib = load()
+    fn = lib.pdeval_program_hoist_flops if hoisted else lib.pdeval_program_flops
     ops = np.ascontiguousarray(ops, dtype=np.int32)
     base = ops.ctypes.data
-    return np.array([lib.pdeval_program_flops(problem_id, base + 4 * int(offsets[i]),
-                                              int(offsets[i + 1] - offsets[i]))
+    return np.array([fn(problem_id, base + 4 * int(offsets[i]), int(offsets[i + 1] - offsets[i]))
                      for i in range(len(offsets) - 1)], dtype=np.float64)
 
 

@@ -1,0 +1,55 @@
+"""CPU tests of the hoisted-prefix cost model (pdeval_program_hoist_flops, include/pdeval.h):
+the part of a program the lean grid passes evaluate 64 times per candidate instead of at every
+point -- its prefix of x alone (once per grid row) or of z alone (once per lane), as
+pdeval_grid.h decode_kernel (PD_HOIST) finds it -- on hand-made programs and on the force-free
+d4 workload the bench tiles.  The device side (same verdicts and residuals with the prefix
+hoisted or not) is tests/test_gpu_parity.py::test_hoisted_prefix_equals_unhoisted."""
+import os
+
+import numpy as np
+import pytest
+
+from pdeval import _lib
+from pdeval import problem_defs as P
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _flops(pd_, s):
+    ops, off, _ = P.compile_strings(pd_, [s])
+    w = np.ascontiguousarray(ops[off[0]:off[1]], dtype=np.int32)
+    lib = _lib.load()
+    ptr = w.ctypes.data
+    return lib.pdeval_program_flops(pd_.problem_id, ptr, w.size), lib.pdeval_program_hoist_flops(pd_.problem_id, ptr, w.size)
+
+
+@pytest.mark.parametrize('s, hoisted', [
+    ('exp(rho)*z', True),          # PUSH_X EXP | ... z: the exponential once per row
+    ('sqrt(rho + 1)*exp(z)', True),
+    ('rho*z', False),              # no heavy opcode before z enters
+    ('exp(rho)', False),           # the whole program is x alone: not hoisted
+    ('exp(z)*rho', True),          # a prefix of z alone: once per lane
+])
+def test_prefix_rule(s, hoisted):
+    pd_ = P.force_free()
+    total, pre = _flops(pd_, s)
+    assert (pre > 0) is hoisted, (s, total, pre)
+    assert 0 <= pre < total - 2 * 160
+
+
+def test_d4_workload_share():
+    """Over the force-free d4 programs (data/force_free_d4_validated.npz): the hoisted part is
+    never more than the program's own opcodes, and it is a sizeable share of the model."""
+    d = np.load(os.path.join(ROOT, 'data', 'force_free_d4_validated.npz'))
+    ops, off = np.ascontiguousarray(d['ops'], dtype=np.int32), d['offsets']
+    lib = _lib.load()
+    base = ops.ctypes.data
+    n = min(len(off) - 1, 20000)
+    tot = pre = 0.0
+    for i in range(n):
+        p, m = base + 4 * int(off[i]), int(off[i + 1] - off[i])
+        f, h = lib.pdeval_program_flops(0, p, m), lib.pdeval_program_hoist_flops(0, p, m)
+        assert 0.0 <= h <= f - 320.0
+        tot += f
+        pre += h
+    assert 0.03 < pre / tot < 0.5, pre / tot
