@@ -117,6 +117,10 @@ struct pdeval_ctx {
     // doubles (env PDEVAL_HOIST=0: none, A/B)
     bool hoist = true;
     double* d_hoist = nullptr;
+    // the lean passes' failing lanes per candidate and grid chunk, cap x chunks words, which
+    // tier 2 re-checks instead of the whole grid (env PDEVAL_TIER2_MASK=0: none, A/B)
+    bool tier2_mask = true;
+    uint64_t* d_fmask = nullptr;
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
     double* d_noise = nullptr;      // fp64 noise bounds at the reference points, cap * 4
     T2Acc* d_t2acc = nullptr;       // tier-2 accumulators, cap entries, zero between launches
@@ -436,6 +440,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_LIST_QUEUE")) c->list_queue = std::max(0, atoi(v));
     if (const char* v = getenv("PDEVAL_LIST_PARTS")) c->list_parts = std::min(16, std::max(1, atoi(v)));
     if (const char* v = getenv("PDEVAL_HOIST")) c->hoist = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_TIER2_MASK")) c->tier2_mask = atoi(v) != 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     if ((e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess)
@@ -472,6 +477,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->d_ddps) (void)hipFree(c->d_ddps);
     if (c->d_dec) (void)hipFree(c->d_dec);
     if (c->d_hoist) (void)hipFree(c->d_hoist);
+    if (c->d_fmask) (void)hipFree(c->d_fmask);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
     if (c->d_t2acc) (void)hipFree(c->d_t2acc);
@@ -633,6 +639,7 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
     int d = 0;
     double f = 0.0, f_at = 0.0;
     bool heavy = false, heavy_at = false;
+    uint32_t msk_at = 0u;
     int64_t at = -1;
     for (int64_t pc = 1; pc < n_words;) {
         const uint32_t w = (uint32_t)ops[pc];
@@ -648,7 +655,7 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
                 pc += len + 1;
                 if (d == 1) {
                     if ((msk[1] & 4u) || msk[1] == 3u) break;
-                    at = pc; f_at = f; heavy_at = heavy;
+                    at = pc; f_at = f; heavy_at = heavy; msk_at = msk[1];
                 }
                 continue;
             }
@@ -677,10 +684,12 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
         pc += len;
         if (d == 1) {
             if ((msk[1] & 4u) || msk[1] == 3u) break;
-            at = pc; f_at = f; heavy_at = heavy;
+            at = pc; f_at = f; heavy_at = heavy; msk_at = msk[1];
         }
     }
-    // (a NEG the decoder folds away is charged like any opcode: the model folds none)
+    // (a NEG the decoder folds away is charged like any opcode: the model folds none; force-free
+    // hoists prefixes of x only, pdeval_grid.h)
+    if (ff && (msk_at & 2u)) return 0.0;
     return (at > 0 && at < n_words && at < (1 << 14) && heavy_at) ? f_at : 0.0;
 }
 
@@ -734,6 +743,10 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
         const int K = c->problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
         HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)cap * (K + 1) * 64 * sizeof(double)));
     }
+    if (c->d_fmask) (void)hipFree(c->d_fmask);
+    c->d_fmask = nullptr;
+    if (c->tier2_mask)
+        HIPCHK(c, hipMalloc(&c->d_fmask, (size_t)cap * c->nx * (c->ny / 64) * sizeof(uint64_t)));
     if (c->d_status) (void)hipFree(c->d_status);
     c->d_status = nullptr;
     HIPCHK(c, hipMalloc(&c->d_status, cap));
@@ -893,6 +906,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.t2acc = c->d_t2acc;
     a.dec = c->d_dec;
     a.hoist = c->nx <= 64 ? c->d_hoist : nullptr;   // (one grid row per lane)
+    a.fmask = c->d_fmask;
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
     // complex-valued ones -> L_CPLX.  Lanes take the candidates sorted by opcode sequence

@@ -767,7 +767,7 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
         cls = PDEVAL_CLS_ACCEPT;
     }
     if (esc && a.esc_list) {
-        esc |= (any_grad ? ESC_ANY_GRAD : 0u) | (nfin > 0 ? ESC_NFIN : 0u);
+        esc |= (any_grad ? ESC_ANY_GRAD : 0u) | (nfin > 0 ? ESC_NFIN : 0u) | (PD_DIVFREE && a.fmask ? ESC_MASK : 0u);
         list_append(a.esc_list, a.esc_count, a.list_capacity, cand | ((int64_t)esc << PD_ESC_SHIFT));
     }
     if (a.out.status) a.out.status[cand] = (uint8_t)cls;
@@ -916,7 +916,10 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
         if (!CX && PD_HOIST && a.hoist && parts == 1) {
             hoist = (int)((dh >> 17) & 0x3fffu);
             hy = (dh >> 31) != 0u;
-            if (hy && a.ny != 64) hoist = 0;   // (one ordinate per lane)
+            // (y alone: one ordinate per lane; Kerr only -- the force-free row loop with the y
+            // form measured 4 % slower in both modes, 132.7 vs 126.5 ms unhoisted, r05_j/r05_i)
+            if (hy && (PROB == PDEVAL_PROBLEM_FORCE_FREE || a.ny != 64)) hoist = 0;
+            if (PROB == PDEVAL_PROBLEM_FORCE_FREE) hy = false;
         }
     }
     if (slow) {
@@ -941,7 +944,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     // (a.nx <= 64, checked by the host, which passes a.hoist = NULL otherwise)
     if constexpr (!CX && PD_HOIST) {
         if (hoist)
-            hoist = hoist_prefix<K, MAXD>(a.dec + beg, hoist, hy, a.gx, a.nx, a.ny, a.ptab,
+            hoist = hoist_prefix<K, MAXD>(a.dec + beg, hoist, PROB != PDEVAL_PROBLEM_FORCE_FREE && hy, a.gx, a.nx, a.ny, a.ptab,
                                           a.hoist + (size_t)cand * (K + 1) * 64, lane, stk, y0, inv_y0);
     }
     GridMax<PROB != PDEVAL_PROBLEM_FORCE_FREE> gm;   // (PD_DIVFREE) the lane's running maximum of q
@@ -1007,7 +1010,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 for (int q = 0; q < W; ++q) {
 #pragma unroll
                     for (int c = 0; c < nc(K); ++c) u[q].c[c] = zero<T>();
-                    if (hy) {
+                    if (PROB != PDEVAL_PROBLEM_FORCE_FREE && hy) {
 #pragma unroll
                         for (int k = 0; k <= K; ++k) u[q].c[ji(0, k)] = cvt<T>(hb[k * 64 + lane]);
                     } else {
@@ -1050,7 +1053,12 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                     gm.add(r.finite, r.res_abs, r.scale);
                     grad_nz = grad_nz | (r.finite & !r.grad_zero);
                     nfin += count_lanes(r.finite);
-                    nbad += count_lanes(r.finite & grid_fails(r.res_abs, r.scale, a.prm.tau_grid));
+                    const uint64_t fm = lane_mask(r.finite & grid_fails(r.res_abs, r.scale, a.prm.tau_grid));
+                    nbad += (int)__popcll(fm);
+                    // the chunk's failing lanes, for tier 2 (a candidate the point stage rejected
+                    // is final and never escalates)
+                    if (a.fmask && (ps & 3) != P0_REJECT && lane == 0)
+                        a.fmask[cand * (int64_t)(a.nx * per_row) + (row + q) * per_row + sl] = fm;
                 } else {
                     if (r.finite) {
                         qmax = fmax(qmax, qv);

@@ -79,6 +79,8 @@ struct KernelArgs {
     struct T2Acc* t2acc;        // tier 2: one accumulator per list entry (pdeval_tier2.h), zeroed
     const int32_t* perm;        // order of pass 0 and the tier-B collect pass (pdeval_sort.hip), or NULL
     int32_t* dec;               // n_words: the programs pre-decoded for the lean grid passes
+    uint64_t* fmask;            // lean passes: per candidate and 64-point grid chunk, the lanes
+                                // that failed the tier-1 test (what tier 2 re-checks); NULL = none
     double* hoist;              // lean passes: per candidate, the pure-x coefficients of its
                                 // x-only prefix at every grid row, [cand][k][row] (pdeval_grid.h
                                 // PD_HOIST); NULL = not hoisted
@@ -153,6 +155,7 @@ enum : uint32_t {
     ESC_GRID_FAIL = 4,  // ... and had more than max_bad failing points
     ESC_ANY_GRAD = 8,   // tier 1 saw a finite point with a non-zero gradient
     ESC_NFIN = 16,      // tier 1 saw at least one finite grid point
+    ESC_MASK = 32,      // ... and recorded its failing points in a.fmask (the lean passes)
 };
 // Point-stage state per candidate (pdeval_point.h).  Bits 0-1: P0_NONE (not decided: malformed
 // program, the grid pass runs its own chunk 0), P0_PASS, P0_REJECT (final).  Flags:
@@ -1006,6 +1009,13 @@ template <bool EXACT> struct GridMax {
 // ------------------------------------------------------------------ wave reductions
 // the lanes where b holds (one s_and with exec of the compare's lane mask; HIP's __ballot(int)
 // first turns the bool into an int in a VGPR and compares it again: 2 VALU more per count)
+__device__ __forceinline__ uint64_t lane_mask(bool b) {
+#ifndef PD_HOST_SIM
+    return __builtin_amdgcn_ballot_w64(b);
+#else
+    return __ballot(b);
+#endif
+}
 __device__ __forceinline__ int count_lanes(bool b) {
 #ifndef PD_HOST_SIM
     return (int)__popcll(__builtin_amdgcn_ballot_w64(b));

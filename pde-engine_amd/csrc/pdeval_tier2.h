@@ -517,12 +517,26 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
         double qmax = 0.0;
         const bool eval_grid = !(flags & ESC_GRID_EVAL) || (flags & ESC_GRID_FAIL);
         if (!eval_grid && part != 0) continue;     // nothing to split: part 0 decides
+        // a grid that tier 1 evaluated and recorded (ESC_MASK): only its failing points are
+        // re-checked -- chunks with none are skipped, the other lanes of a chunk count nothing.
+        // Its q_grid, non-finite count and finite flag are tier 1's (outputs written by pass 1).
+        const bool masked = (flags & ESC_GRID_EVAL) && (flags & ESC_MASK) && a.fmask;
         if (eval_grid) {
             const int per_row = a.ny >> 6;
             const int nchunks = a.nx * per_row;
             const int ch0 = (int)((int64_t)nchunks * part / PARTS);
             const int ch1 = (int)((int64_t)nchunks * (part + 1) / PARTS);
+            // (packing the failing points 64 to a batch, x per lane, measured slower: force-free
+            // tier 2 7.9 vs 6.5 ms, Kerr 2.1 vs 1.3 ms, profiles/r05_n_ab_*.log)
             for (int ch = ch0; ch < ch1; ++ch) {
+                uint64_t m = ~0ull;
+                if (masked) {
+                    const uint64_t v = a.fmask[cand * (int64_t)nchunks + ch];
+                    m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+                    if (m == 0ull) continue;
+                }
+                const bool sel = (m >> lane) & 1ull;
                 const int row = ch / per_row, sl = ch - row * per_row;
                 const int p = a.n_ref + row * a.ny + sl * 64 + lane;
                 const double x = rd_sf64(a.gx + row);
@@ -540,7 +554,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
                 const double qv = scaled(r.res_abs, r.scale);
                 qmax = fmax(qmax, qv);
                 if (!r.grad_zero) grad_nz = true;
-                if (grid_fails(r.res_abs, r.scale, a.prm.tau_grid)) {
+                if (sel && grid_fails(r.res_abs, r.scale, a.prm.tau_grid)) {
                     ++nb1;
                     if (r.res_abs > a.prm.noise_kappa * residual_noise<PROB, T>(u.c, e, x, kc, r.scale, a.prm.omega2)) ++nb2;
                 }
@@ -587,7 +601,7 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
         const bool pconst = a.pstate && (a.pstate[cand] & P0_CONST);
         const bool any_grad = (grad_any || (flags & ESC_ANY_GRAD)) && !pconst;
         if (lane == 0) {
-            const bool has_fin = eval_grid ? nfin > 0 : (flags & ESC_NFIN) != 0;
+            const bool has_fin = eval_grid && !masked ? nfin > 0 : (flags & ESC_NFIN) != 0;
             const bool structural = (PROB != PDEVAL_PROBLEM_FORCE_FREE) || (hdr & PDEVAL_FLAG_NOCOORD);
             int cls;
             if (!any_grad && (has_fin || pconst) && structural) cls = PDEVAL_CLS_ZERO_GRADIENT;

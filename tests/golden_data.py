@@ -150,6 +150,7 @@ FF_D5_SYMBOLIC_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))'}
 # them and agrees (tests/test_symbolic_replay.py::test_strict_mode_every_decided_row):
 #   the reference's false negatives (det == 0, SymPy cannot reduce it) ...
 FF_OFF_MODE_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))', 'sqrt(square(inv(rho))/(1 - z))',
+                          'exp_neg(rho/z - pow_neg_3_2(exp(rho/z)))',   # (d5 s7000: a function of rho/z)
                           # ... and squares under a fractional power that the NONSMOOTH2D rule
                           # rejects but SymPy's Abs form lets the reference prove
                           'pow_neg_3_2(square(rho - z))', 'pow_neg_3_2(square(rho**2 + z**2 - z - 1))',

@@ -596,7 +596,7 @@ def test_hoisted_prefix_equals_unhoisted(pid, data, n):
     ops, off = d['ops'], d['offsets']
     if n is not None and len(off) - 1 > n:
         ops, off = WL.gather_programs(ops, off, np.arange(n))
-    assert (WL.flops_per_program(pid, ops, off, hoisted=True) > 0).mean() > 0.2
+    assert (WL.flops_per_program(pid, ops, off, hoisted=True) > 0).mean() > 0.1   # (FF 44 %, Kerr 12 %)
     on = _validate_env(pid, ops, off, {'PDEVAL_HOIST': '1'})
     off_ = _validate_env(pid, ops, off, {'PDEVAL_HOIST': '0'})
     for k in ('status', 'verdict', 'n_bad', 'n_nonfinite', 'q_ref', 'res_ref', 'fingerprint'):
@@ -608,3 +608,24 @@ def test_hoisted_prefix_equals_unhoisted(pid, data, n):
     assert np.array_equal(np.isfinite(a), np.isfinite(b))
     rel = np.abs(a[both] - b[both]) / np.maximum(np.abs(b[both]), 1e-300)
     assert rel.max(initial=0.0) <= 1e-13 and (rel > 0).mean() < 1e-3, (rel.max(initial=0.0), (rel > 0).sum())
+
+
+@pytest.mark.parametrize('pid, data, n', [(0, 'force_free_d4_validated.npz', None),
+                                          (1, 'kerr_magnetosphere_d4_stream.npz', 200000)])
+def test_tier2_masked_equals_full(pid, data, n):
+    """Tier 2 re-checks only the grid points tier 1 failed (the lean passes' per-chunk lane masks,
+    a.fmask / ESC_MASK) instead of the whole grid: against PDEVAL_TIER2_MASK=0 every class,
+    verdict, grid count, maximum and residual of the force-free d4 workload and of 200,000
+    Kerr d4 programs is the same.  (A point tier 1 passed cannot be a tier-2 failure: tier 2's
+    own tier-1 test is the same arithmetic on the same values.)"""
+    from pdeval import workload as WL
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'data', data))
+    ops, off = d['ops'], d['offsets']
+    if n is not None and len(off) - 1 > n:
+        ops, off = WL.gather_programs(ops, off, np.arange(n))
+    on = _validate_env(pid, ops, off, {'PDEVAL_TIER2_MASK': '1'})
+    off_ = _validate_env(pid, ops, off, {'PDEVAL_TIER2_MASK': '0'})
+    for k in ('status', 'verdict', 'n_bad', 'n_nonfinite', 'q_grid', 'q_ref', 'res_ref', 'fingerprint'):
+        if k in on:
+            assert np.array_equal(on[k], off_[k], equal_nan=on[k].dtype.kind == 'f'), \
+                (k, np.flatnonzero(np.any((on[k] != off_[k]).reshape(len(on[k]), -1), axis=1))[:10])

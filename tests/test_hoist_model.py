@@ -23,18 +23,20 @@ def _flops(pd_, s):
     return lib.pdeval_program_flops(pd_.problem_id, ptr, w.size), lib.pdeval_program_hoist_flops(pd_.problem_id, ptr, w.size)
 
 
-@pytest.mark.parametrize('s, hoisted', [
-    ('exp(rho)*z', True),          # PUSH_X EXP | ... z: the exponential once per row
-    ('sqrt(rho + 1)*exp(z)', True),
-    ('rho*z', False),              # no heavy opcode before z enters
-    ('exp(rho)', False),           # the whole program is x alone: not hoisted
-    ('exp(z)*rho', True),          # a prefix of z alone: once per lane
+@pytest.mark.parametrize('prob, s, hoisted', [
+    ('force_free', 'exp(rho)*z', True),          # PUSH_X EXP | ... z: the exponential once per row
+    ('force_free', 'sqrt(rho + 1)*exp(z)', True),
+    ('force_free', 'rho*z', False),              # no heavy opcode before z enters
+    ('force_free', 'exp(rho)', False),           # the whole program is x alone: not hoisted
+    ('force_free', 'exp(z)*rho', False),         # a prefix of z alone: hoisted for Kerr only
+    ('kerr_magnetosphere', 'exp(x)*r', True),    # Kerr's lane coordinate x: once per lane
+    ('kerr_magnetosphere', 'sqrt(r + 1)*x', True),
 ])
-def test_prefix_rule(s, hoisted):
-    pd_ = P.force_free()
+def test_prefix_rule(prob, s, hoisted):
+    pd_ = P.get(prob)
     total, pre = _flops(pd_, s)
     assert (pre > 0) is hoisted, (s, total, pre)
-    assert 0 <= pre < total - 2 * 160
+    assert 0 <= pre < total - (2 * 160 if pd_.problem_id == 0 else 16)
 
 
 def test_d4_workload_share():
