@@ -142,7 +142,7 @@ FF_COUNT_SLACK = {
 # long enough for the reference to expand it (validator.py:407-426, "expanded det != 0") while
 # SymPy leaves the sqrt(rho/z) terms un-merged -- are reproduced by the 'replay' mode
 # (pdeval/symbolic.py); the default mode gives the true verdict.
-FF_D5 = ('ff_d5_s400.jsonl', 'ff_d5_s4000_t20.jsonl')
+FF_D5 = ('ff_d5_s400.jsonl', 'ff_d5_s4000_t20.jsonl', 'ff_d5_s7000_t20.jsonl')
 FF_D5_SYMBOLIC_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))'}
 # Every decided force-free fixture row on which the default mode ('off': the grid's det == 0
 # and the structural rules) and the reference's verdict differ -- all decided in the reference's
