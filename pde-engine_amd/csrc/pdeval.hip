@@ -116,7 +116,9 @@ struct pdeval_ctx {
     // the hoisted x-only prefixes of the lean passes (pdeval_grid.h PD_HOIST): cap x (K + 1) x 64
     // doubles (env PDEVAL_HOIST=0: none, A/B)
     bool hoist = true;
+    bool hoist_sub = true;              // env PDEVAL_HOIST_SUB=0: no hoisted segments (A/B)
     double* d_hoist = nullptr;
+    int32_t* d_hseg = nullptr;          // the decoder's hoisted segments, cap x 4 words
     // the lean passes' failing lanes per candidate and grid chunk, cap x chunks words, which
     // tier 2 re-checks instead of the whole grid (env PDEVAL_TIER2_MASK=0: none, A/B)
     bool tier2_mask = true;
@@ -440,6 +442,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_LIST_QUEUE")) c->list_queue = std::max(0, atoi(v));
     if (const char* v = getenv("PDEVAL_LIST_PARTS")) c->list_parts = std::min(16, std::max(1, atoi(v)));
     if (const char* v = getenv("PDEVAL_HOIST")) c->hoist = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_HOIST_SUB")) c->hoist_sub = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_TIER2_MASK")) c->tier2_mask = atoi(v) != 0;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
@@ -477,6 +480,7 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->d_ddps) (void)hipFree(c->d_ddps);
     if (c->d_dec) (void)hipFree(c->d_dec);
     if (c->d_hoist) (void)hipFree(c->d_hoist);
+    if (c->d_hseg) (void)hipFree(c->d_hseg);
     if (c->d_fmask) (void)hipFree(c->d_fmask);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
@@ -638,9 +642,29 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
     uint32_t msk[PDEVAL_MAX_STACK + 2] = {};
     int d = 0;
     double f = 0.0, f_at = 0.0;
-    bool heavy = false, heavy_at = false;
+    bool heavy = false, heavy_at = false, alive = true, cplx = false;
     uint32_t msk_at = 0u;
     int64_t at = -1;
+    // Kerr's hoisted segment (pdeval_grid.h PD_HOIST_SUB): depth-2 segments of one coordinate
+    // holding a heavy opcode, at most 31 words, after the prefix; the one with most heavy opcodes
+    struct Seg { int64_t hs, he; int nh; double f; bool y; };
+    Seg segs[4];
+    int nseg = 0, seg_nh = 0;
+    int64_t seg_start = -1;
+    double seg_f0 = 0.0;
+    auto heavy_op = [](uint32_t op) {
+        return op == PDOP_MUL || op == PDOP_DIV || op == PDOP_RDIV || op == PDOP_RDIVC || op == PDOP_POWN ||
+               op == PDOP_POW || op == PDOP_SQRT || op == PDOP_EXP || op == PDOP_LOG || op == PDOP_MUL_P ||
+               op == PDOP_DIV_P || op == PDOP_RDIV_P || op == PDOP_DIV_X;
+    };
+    auto track_prefix = [&](int64_t pc_next) {
+        if (!alive || d != 1) return;
+        if ((msk[1] & 4u) || msk[1] == 3u) {
+            alive = false;
+            return;
+        }
+        at = pc_next; f_at = f; heavy_at = heavy; msk_at = msk[1];
+    };
     for (int64_t pc = 1; pc < n_words;) {
         const uint32_t w = (uint32_t)ops[pc];
         const uint32_t op = w & 0xffu;
@@ -651,12 +675,10 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
             if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || op2 == PDOP_MUL_P) {
                 ++d;
                 msk[d] = (op2 == PDOP_MUL_Y || (op2 == PDOP_MUL_P && ((w2 >> 16) & 1u))) ? 2u : 1u;
+                if (d == 2) { seg_start = pc; seg_nh = 0; seg_f0 = f; }
                 f += op_flops(ff, w) + op_flops(ff, w2);
                 pc += len + 1;
-                if (d == 1) {
-                    if ((msk[1] & 4u) || msk[1] == 3u) break;
-                    at = pc; f_at = f; heavy_at = heavy; msk_at = msk[1];
-                }
+                track_prefix(pc);
                 continue;
             }
         }
@@ -664,10 +686,16 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
             case PDOP_PUSH_X: msk[++d] = 1u; break;
             case PDOP_PUSH_Y: msk[++d] = 2u; break;
             case PDOP_PUSH_C: msk[++d] = 0u; break;
-            case PDOP_PUSH_I: msk[++d] = 4u; break;
+            case PDOP_PUSH_I: msk[++d] = 4u; cplx = true; break;
             case PDOP_PUSH_P: msk[++d] = on_y ? 2u : 1u; break;
             case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: case PDOP_MUL: case PDOP_DIV: case PDOP_RDIV:
                 --d;
+                if (d == 1 && seg_start >= 0) {
+                    const uint32_t m2 = msk[2];
+                    if (seg_nh > 0 && m2 <= 2u && pc - seg_start <= 31 && nseg < 4)
+                        segs[nseg++] = {seg_start, pc, seg_nh, f - seg_f0, m2 == 2u};
+                    seg_start = -1;
+                }
                 msk[d] |= msk[d + 1];
                 break;
             case PDOP_ADD_X: case PDOP_SUB_X: case PDOP_MUL_X: case PDOP_DIV_X: msk[d] |= 1u; break;
@@ -677,20 +705,31 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
                 break;
             default: break;
         }
-        f += op_flops(ff, w);
-        heavy = heavy || op == PDOP_MUL || op == PDOP_DIV || op == PDOP_RDIV || op == PDOP_RDIVC ||
-                op == PDOP_POWN || op == PDOP_POW || op == PDOP_SQRT || op == PDOP_EXP || op == PDOP_LOG ||
-                op == PDOP_MUL_P || op == PDOP_DIV_P || op == PDOP_RDIV_P || op == PDOP_DIV_X;
-        pc += len;
-        if (d == 1) {
-            if ((msk[1] & 4u) || msk[1] == 3u) break;
-            at = pc; f_at = f; heavy_at = heavy; msk_at = msk[1];
+        if ((op == PDOP_PUSH_X || op == PDOP_PUSH_Y || op == PDOP_PUSH_C || op == PDOP_PUSH_I ||
+             op == PDOP_PUSH_P) && d == 2) {
+            seg_start = pc; seg_nh = 0; seg_f0 = f;
         }
+        f += op_flops(ff, w);
+        heavy = heavy || heavy_op(op);
+        if (d >= 2 && heavy_op(op)) ++seg_nh;
+        pc += len;
+        track_prefix(pc);
     }
     // (a NEG the decoder folds away is charged like any opcode: the model folds none; force-free
     // hoists prefixes of x only, pdeval_grid.h)
-    if (ff && (msk_at & 2u)) return 0.0;
-    return (at > 0 && at < n_words && at < (1 << 14) && heavy_at) ? f_at : 0.0;
+    double h = 0.0;
+    int64_t hp = 0;
+    if (!(ff && (msk_at & 2u)) && at > 0 && at < n_words && at < (1 << 14) && heavy_at) {
+        h = f_at;
+        hp = at;
+    }
+    if (!ff && !cplx) {
+        int best = -1;
+        for (int k = 0; k < nseg; ++k)
+            if (segs[k].hs >= hp && (best < 0 || segs[k].nh > segs[best].nh)) best = k;
+        if (best >= 0) h += segs[best].f;
+    }
+    return h;
 }
 
 // ---------------------------------------------------------------------------- launches
@@ -739,9 +778,14 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     HIPCHK(c, hipMalloc(&c->d_ddps, cap));
     if (c->d_hoist) (void)hipFree(c->d_hoist);
     c->d_hoist = nullptr;
+    if (c->d_hseg) (void)hipFree(c->d_hseg);
+    c->d_hseg = nullptr;
     if (c->hoist) {
+        // per candidate: the prefix's pure coefficients (K + 1 rows of 64) and the segment's
+        // whole jet (nc(K) rows of 64) -- pd::hoist_stride
         const int K = c->problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
-        HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)cap * (K + 1) * 64 * sizeof(double)));
+        HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)cap * pd::hoist_stride(K) * sizeof(double)));
+        HIPCHK(c, hipMalloc(&c->d_hseg, (size_t)cap * 4 * sizeof(int32_t)));
     }
     if (c->d_fmask) (void)hipFree(c->d_fmask);
     c->d_fmask = nullptr;
@@ -906,6 +950,7 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.t2acc = c->d_t2acc;
     a.dec = c->d_dec;
     a.hoist = c->nx <= 64 ? c->d_hoist : nullptr;   // (one grid row per lane)
+    a.hseg = a.hoist && c->hoist_sub ? c->d_hseg : nullptr;
     a.fmask = c->d_fmask;
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,

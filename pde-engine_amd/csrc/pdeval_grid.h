@@ -69,12 +69,19 @@ constexpr uint64_t kVarMask = op_bit(PDOP_MUL_X) | op_bit(PDOP_MUL_Y) | op_bit(P
 //                              the lean passes cannot take it (lean_prescan<3> fails)
 //   at each opcode position    op (bits 0-7), the word's own bits 8-16 (POWN / coordinate power
 //                              n, axis), the dispatch group (17-19), last-opcode bit (20), the
-//                              distance to the next opcode (21-23: 1, 3 or 5), and the dispatch
-//                              group again as one bit of 24-29 (PD_ONEHOT: one bit test each)
+//                              distance to the next opcode (21-25: 1, 3 or 5, more after folded
+//                              NEGs, up to 31 over a hoisted segment), and the dispatch group
+//                              again as one bit of 26-31 (PD_ONEHOT: one bit test each)
 //   after an immediate opcode  the immediate as a double (low word first), a problem constant
 //                              (PDEVAL_IMM_PRM) already resolved to the grid stage's value
 // The lean passes then read only the decoded array.
 enum : uint32_t { DG_PUSH = 0, DG_CHEAP = 1, DG_POP = 2, DG_BIN = 3, DG_VAR = 4, DG_OTHER = 5 };
+constexpr int DEC_DIST = 21;          // distance field: bits 21-25
+constexpr uint32_t DEC_DIST_MAX = 31u;
+constexpr int DEC_ONEHOT = 26;        // one-hot group: bits 26-31
+// decoded-only opcode: push the hoisted jet of a single-coordinate segment (PD_HOIST_SUB); its
+// distance steps over the segment to the binary opcode that consumes it
+constexpr uint32_t DOP_PUSH_H = 40u;
 #ifndef PD_KERR_NOMIX
 #define PD_KERR_NOMIX 1
 #endif
@@ -85,7 +92,7 @@ enum : uint32_t { DG_PUSH = 0, DG_CHEAP = 1, DG_POP = 2, DG_BIN = 3, DG_VAR = 4,
 #define PD_FUSE_PUSHC 1
 #endif
 __device__ __forceinline__ uint32_t dec_group(uint64_t b) {
-    if (b & (kPushMask | op_bit(PDOP_PUSH_I))) return DG_PUSH;
+    if (b & (kPushMask | op_bit(PDOP_PUSH_I) | op_bit((int)DOP_PUSH_H))) return DG_PUSH;
     if (b & kCheapMask) return DG_CHEAP;
     if (b & kPOpMask) return DG_POP;
     if (b & kBinMask) return DG_BIN;
@@ -136,6 +143,14 @@ __device__ __forceinline__ bool neg_fold_ok(const int32_t* prog, int plen) {
 #ifndef PD_HOIST
 #define PD_HOIST 1
 #endif
+// single-coordinate segments (a right operand: the PUSH_Y SQRT of PUSH_X EXP PUSH_Y SQRT MUL)
+// hoisted the same way, as a push of the stored jet inside the row loop -- Kerr only: same box,
+// 2^21, Kerr 25.38 -> 26.04 M cand/s, but force-free 13.43 -> 13.29 (the push's code in its
+// interpreter cost more than the segments saved; profiles/r05_p_ab_*.log)
+#ifndef PD_HOIST_SUB
+#define PD_HOIST_SUB 1
+#endif
+template <int PROB> constexpr bool hoist_sub() { return PD_HOIST_SUB && PROB != PDEVAL_PROBLEM_FORCE_FREE; }
 constexpr uint64_t kHeavyMask = op_bit(PDOP_MUL) | op_bit(PDOP_DIV) | op_bit(PDOP_RDIV) | op_bit(PDOP_RDIVC) |
                                 op_bit(PDOP_POWN) | op_bit(PDOP_POW) | op_bit(PDOP_SQRT) | op_bit(PDOP_EXP) |
                                 op_bit(PDOP_LOG) | op_bit(PDOP_MUL_P) | op_bit(PDOP_DIV_P) | op_bit(PDOP_RDIV_P) |
@@ -171,6 +186,11 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     uint32_t msk[5] = {0u, 0u, 0u, 0u, 0u};
     int hoist_last = -1;
     bool hoist_alive = true, heavy = false, hoist_heavy = false, hoist_y = false;
+    // PD_HOIST_SUB: the depth-2 segments (a push from depth 1 to the binary opcode back to 1)
+    // whose value depends on one coordinate alone and that hold a heavy opcode
+    int seg_start = -1, seg_nh = 0, nseg = 0;
+    int sg_hs[4] = {0, 0, 0, 0}, sg_he[4] = {0, 0, 0, 0}, sg_nh[4] = {0, 0, 0, 0};
+    bool sg_y[4] = {false, false, false, false};
     const bool fold = PD_FOLD_NEG && ok && neg_fold_ok(prog, plen);
     while (ok && pc < plen) {
         const uint32_t w = (uint32_t)prog[pc];
@@ -217,10 +237,14 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
             const uint32_t w2 = (uint32_t)prog[pc + len];
             const uint32_t op2 = w2 & 0xffu;
             if (op2 == PDOP_MUL_X || op2 == PDOP_MUL_Y || (PD_FUSE_PUSHC == 1 && op2 == PDOP_MUL_P)) {
-                dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << 21) |
-                                    (1u << (24 + DG_PUSH)));
+                dec[pc] = (int32_t)(op2 | (w2 & 0x1ff00u) | (DG_PUSH << 17) | ((uint32_t)(len + 1) << DEC_DIST) |
+                                    (1u << (DEC_ONEHOT + DG_PUSH)));
                 sg[d] = 1;
                 msk[d] = (op2 == PDOP_MUL_Y || (op2 == PDOP_MUL_P && ((w2 >> 16) & 1u))) ? 2u : 1u;
+                if (d == 2) {
+                    seg_start = pc;
+                    seg_nh = 0;
+                }
                 hoist_track(d, msk, pc, heavy, hoist_alive, hoist_last, hoist_heavy, hoist_y);
                 last = pc;
                 pc += len + 1;
@@ -243,9 +267,9 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
         if (fold) {
             if (op == PDOP_NEG) {
                 const uint32_t pw = last >= 0 ? (uint32_t)dec[last] : 0u;
-                if (last >= 0 && ((pw >> 21) & 7u) + 1u <= 7u) {
+                if (last >= 0 && ((pw >> DEC_DIST) & DEC_DIST_MAX) + 1u <= DEC_DIST_MAX) {
                     sg[d] = -sg[d];
-                    dec[last] = (int32_t)(pw + (1u << 21));   // the previous opcode steps over it
+                    dec[last] = (int32_t)(pw + (1u << DEC_DIST));   // the previous opcode steps over it
                     pc += 1;
                     continue;
                 }
@@ -293,12 +317,28 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
             }
         }
         dec[pc] = (int32_t)(dop | (w & 0x1ff00u & ((kImmMask & b) ? 0u : ~0u)) | (dec_group(op_bit((int)dop)) << 17) |
-                            ((uint32_t)len << 21) | (1u << (24 + dec_group(op_bit((int)dop)))));
+                            ((uint32_t)len << DEC_DIST) | (1u << (DEC_ONEHOT + dec_group(op_bit((int)dop)))));
         // (masks follow the original opcode: a folded sign does not change what it depends on)
         if ((kPushMask | op_bit(PDOP_PUSH_I)) & b) {
             msk[d] = op == PDOP_PUSH_X ? 1u : op == PDOP_PUSH_Y ? 2u : op == PDOP_PUSH_I ? 4u
                    : op == PDOP_PUSH_P ? (((w >> 16) & 1u) ? 2u : 1u) : 0u;
+            if (d == 2) {
+                seg_start = pc;
+                seg_nh = 0;
+            }
         } else if (kBinMask & b) {
+            if (d == 1 && seg_start >= 0) {   // a depth-2 segment closes here
+                const uint32_t m2 = msk[2];
+                if (seg_nh > 0 && (m2 == 0u || m2 == 1u || m2 == 2u) && pc - seg_start <= (int)DEC_DIST_MAX &&
+                    nseg < 4) {
+                    sg_hs[nseg] = seg_start;
+                    sg_he[nseg] = pc;
+                    sg_nh[nseg] = seg_nh;
+                    sg_y[nseg] = m2 == 2u;
+                    ++nseg;
+                }
+                seg_start = -1;
+            }
             msk[d] |= msk[d + 1];
         } else if ((kPOpMask & b) || op == PDOP_ADD_X || op == PDOP_SUB_X || op == PDOP_MUL_X ||
                    op == PDOP_DIV_X || op == PDOP_ADD_Y || op == PDOP_SUB_Y || op == PDOP_MUL_Y ||
@@ -308,6 +348,7 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
             msk[d] |= on_y ? 2u : 1u;
         }
         heavy = heavy || (kHeavyMask & b);
+        if (d >= 2 && (kHeavyMask & b)) ++seg_nh;
         hoist_track(d, msk, pc, heavy, hoist_alive, hoist_last, hoist_heavy, hoist_y);
         last = pc;
         pc += len;
@@ -318,11 +359,35 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     // is final now -- a folded NEG after it extends that distance), or 0 for none
     uint32_t hp = 0u;
     if (PD_HOIST && ok && hoist_last >= 0 && hoist_heavy) {
-        const uint32_t at = (uint32_t)hoist_last + (((uint32_t)dec[hoist_last] >> 21) & 7u);
+        const uint32_t at = (uint32_t)hoist_last + (((uint32_t)dec[hoist_last] >> DEC_DIST) & DEC_DIST_MAX);
         if (at < (uint32_t)plen && at < (1u << 14)) hp = at;   // (not a whole program of x alone)
     }
     dec[0] = ok ? (int32_t)(((uint32_t)dmax << 8) | (sg[1] < 0 ? 1u << 16 : 0u) | (hp << 17) |
                             (hp && hoist_y ? 1u << 31 : 0u)) : (int32_t)0xff;
+    // the hoisted segment: the heaviest one after the prefix (force-free: x alone), its first
+    // opcode word replaced by DOP_PUSH_H, the original kept in a.hseg with its span and kind
+    if (a.hseg) {
+        int best = -1;
+        // (not for the complex pass's candidates: the complex interpreter hoists nothing)
+        const bool cplx = (hdr & PDEVAL_FLAG_COMPLEX) || (a.pstate && (a.pstate[cand] & P0_CPLX));
+        if (hoist_sub<PROB>() && ok && !cplx)
+            for (int k = 0; k < nseg; ++k)
+                if (sg_hs[k] >= (int)hp && (!sg_y[k] || (PROB != PDEVAL_PROBLEM_FORCE_FREE && a.ny == 64)) &&
+                    (best < 0 || sg_nh[k] > sg_nh[best]))
+                    best = k;
+        int32_t* hs = a.hseg + 4 * cand;
+        if (best >= 0) {
+            const int at = sg_hs[best], to = sg_he[best];
+            hs[0] = dec[at];
+            hs[1] = at;
+            hs[2] = to;
+            hs[3] = sg_y[best] ? 1 : 0;
+            dec[at] = (int32_t)(DOP_PUSH_H | (DG_PUSH << 17) | ((uint32_t)(to - at) << DEC_DIST) |
+                                (1u << (DEC_ONEHOT + DG_PUSH)));
+        } else {
+            hs[1] = 0;
+        }
+    }
 }
 
 // ---- coordinate-power tables.  A coordinate power v**n (PDOP_*_P) enters the interpreter as
@@ -486,11 +551,17 @@ template <class T, int K, int W, int MAXD> struct Lean {
     // pc0: the first opcode to run -- 1, or the position after a hoisted prefix (PD_HOIST), with
     // acc holding the prefix's value at stack depth 1.  PRE (XL: x per lane): stop before the
     // opcode at `stop` (the hoisted prefix alone).
+    // h2 (PD_HOIST_SUB): the candidate's hoisted segment jet, [coefficient][row or lane]; its
+    // DOP_PUSH_H pushes row h2row + q (clamped to h2last) or, h2y, the lane's own.  w0 / fresh:
+    // the pre-phase of a segment starts at its first opcode with the original word w0 and an
+    // empty stack.
     template <bool XL = false, bool PRE = false>
     static __device__ __forceinline__ void run(const int32_t* dec, const double (&x)[W], double y,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
                                                T* stk, int lane, const PowTab<W>& pt, int pc0 = 1,
-                                               int stop = 0) {
+                                               int stop = 0, const double* h2 = nullptr, int h2row = 0,
+                                               int h2last = 0, bool h2y = false, uint32_t w0 = 0u,
+                                               bool fresh = false) {
         // MAXD = 3 (pass 2): the upper of the two operand slots lives in VGPRs, the lower in
         // LDS -- two LDS slots of W = 2 Kerr jets (12 KiB per wave) held pass 2 at ~3 waves
         // per SIMD; with one, VGPRs set the occupancy
@@ -499,21 +570,21 @@ template <class T, int K, int W, int MAXD> struct Lean {
         // an opcode word and the two after it (its f64 immediate, when it has one) are read
         // together, one op ahead, so an op's immediate is in SGPRs when its turn comes instead
         // of costing a dependent scalar load (dec[] is padded by 4 words past its end)
-        uint32_t w = rd_word(dec + pc0);
+        uint32_t w = w0 ? w0 : rd_word(dec + pc0);
         double imm = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + pc0 + 1) : 0.0;
-        bool first = pc0 == 1;
-        int d = pc0 == 1 ? 0 : 1;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
+        bool first = fresh || pc0 == 1;
+        int d = first ? 0 : 1;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
         for (;;) {
             const uint32_t op = w & 0xffu;
             const uint32_t grp = (w >> 17) & 7u;
             // group tests: a bit test on the one-hot copy (s_bitcmp + branch) or a compare of
             // the 3-bit field (extract + compare + branch)
             auto in_grp = [&](uint32_t g) -> bool {
-                if constexpr (PD_ONEHOT) return (w >> (24 + g)) & 1u;
+                if constexpr (PD_ONEHOT) return (w >> (DEC_ONEHOT + g)) & 1u;
                 else return grp == g;
             };
             const bool more = !((w >> 20) & 1u);
-            const int npc = pc + (int)((w >> 21) & 7u);
+            const int npc = pc + (int)((w >> DEC_DIST) & DEC_DIST_MAX);
             // the next opcode word is fetched before this op's arithmetic (its scalar-load
             // latency hides under it); after the last op the three words past the program are
             // read and ignored -- they exist: the decoded array is padded by 4 words
@@ -594,6 +665,15 @@ template <class T, int K, int W, int MAXD> struct Lean {
                     if constexpr (Real<T>::cplx_pass) {
 #pragma unroll
                         for (int q = 0; q < W; ++q) O::set_const(acc[q], imag_unit<T>());
+                    }
+                } else if (!Real<T>::cplx_pass && PD_HOIST_SUB && K != 4 && op == DOP_PUSH_H) {
+                    if constexpr (!Real<T>::cplx_pass && PD_HOIST_SUB && K != 4) {   // (Kerr only)
+#pragma unroll
+                        for (int q = 0; q < W; ++q) {
+                            const int at = h2y ? lane : min(h2row + q, h2last);
+#pragma unroll
+                            for (int c = 0; c < NCJ; ++c) acc[q].c[c] = live(c) ? h2[c * 64 + at] : zero<T>();
+                        }
                     }
                 } else {
                     const double c = cimm;
@@ -828,22 +908,19 @@ template <int PROB, int MAXD, class T = double> constexpr size_t grid_lds(int wa
     return (size_t)waves * L::LDS_SLOTS * L::SLOT * sizeof(T);
 }
 
-// The hoisted prefix (PD_HOIST) of one candidate.  x alone: lane r = grid row r, its pure-x
-// coefficients into hb[k][row]; y alone: lane j at its own ordinate (the prefix reads no x),
-// the pure-y coefficients into hb[k][j].  Returns `hoist`, or 0 when some lane carries a
-// non-zero coefficient outside those (a non-finite value: the row loop then runs the whole
-// program).  (PD_HOIST_NOINLINE=1, out of line: the call frame took 608 B of scratch)
-#ifndef PD_HOIST_NOINLINE
-#define PD_HOIST_NOINLINE 0
-#endif
-template <int K, int MAXD>
-#if PD_HOIST_NOINLINE
-__device__ __noinline__
-#else
-__device__ __forceinline__
-#endif
-int hoist_prefix(const int32_t* dec, int hoist, bool hy, const double* gx, int nx, int ny, const double* ptab,
-                 double* hb, int lane, double* stk, double y0, double inv_y0) {
+// The hoisted parts (PD_HOIST) of one candidate, in one loop so that the interpreter is inlined
+// once.  Job 0, the prefix: x alone, lane r = grid row r, its pure-x coefficients into
+// hb[k][row]; y alone, lane j at its own ordinate (the prefix reads no x), the pure-y ones into
+// hb[k][j]; returns 0 for `hoist` when some lane carries a non-zero coefficient outside those (a
+// non-finite value: the row loop then runs the prefix itself).  Job 1, the segment
+// (PD_HOIST_SUB): from its first opcode (original word w0) with an empty stack to the opcode
+// before the binary one that consumes it, every coefficient into hb2[c][row or lane] -- the
+// whole jet, so no lane's value can differ from the one the row loop would compute.
+template <int K, int MAXD, bool SUB>
+__device__ __forceinline__ void hoist_parts(const int32_t* dec, int& hoist, bool hy, int h_at, int h_to, uint32_t h_w0,
+                                            bool h_y, const double* gx, int nx, int ny, const double* ptab,
+                                            double* hb, double* hb2, int lane, double* stk, double y0,
+                                            double inv_y0) {
     using L1 = Lean<double, K, 1, MAXD>;
     const int r = min(lane, nx - 1);
     const double xl[1] = {gx[r]}, ixl[1] = {gx[nx + r]};
@@ -853,21 +930,33 @@ int hoist_prefix(const int32_t* dec, int hoist, bool hy, const double* gx, int n
     p1.ny = ny;
     p1.px[0] = ptab + (size_t)r * (K + 1);
     p1.py = ptab + (size_t)PTAB_N * nx * (K + 1) + lane;
-    typename L1::J h[1];
-    L1::template run<true, true>(dec, xl, y0, ixl, inv_y0, h, stk, lane, p1, 1, hoist);
-    bool dirty = false;
+#pragma unroll 1
+    for (int job = 0; job < (SUB ? 2 : 1); ++job) {
+        if (job == 0 ? hoist == 0 : h_at == 0) continue;   // (uniform)
+        typename L1::J h[1];
+        L1::template run<true, true>(dec, xl, y0, ixl, inv_y0, h, stk, lane, p1, job ? h_at : 1, job ? h_to : hoist,
+                                     nullptr, 0, 0, false, job ? h_w0 : 0u, job != 0);
+        if (job == 0) {
+            bool dirty = false;
 #pragma unroll
-    for (int c = 0; c < nc(K); ++c) {
-        bool pure = false;
+            for (int c = 0; c < nc(K); ++c) {
+                bool pure = false;
 #pragma unroll
-        for (int k = 0; k <= K; ++k) pure = pure || c == (hy ? ji(0, k) : ji(k, 0));
-        if (!pure) dirty = dirty || !(h[0].c[c] == 0.0);
+                for (int k = 0; k <= K; ++k) pure = pure || c == (hy ? ji(0, k) : ji(k, 0));
+                if (!pure) dirty = dirty || !(h[0].c[c] == 0.0);
+            }
+            if (__any(dirty)) {
+                hoist = 0;
+                continue;
+            }
+#pragma unroll
+            for (int k = 0; k <= K; ++k) hb[k * 64 + lane] = h[0].c[hy ? ji(0, k) : ji(k, 0)];
+        } else {
+#pragma unroll
+            for (int c = 0; c < nc(K); ++c) hb2[c * 64 + lane] = h[0].c[c];
+        }
     }
-    if (__any(dirty)) return 0;
-#pragma unroll
-    for (int k = 0; k <= K; ++k) hb[k * 64 + lane] = h[0].c[hy ? ji(0, k) : ji(k, 0)];
     __threadfence_block();   // the rows read other lanes' values
-    return hoist;
 }
 
 // The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots, jets
@@ -909,10 +998,24 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     uint32_t u_sgn = 0u;   // a sign the decoder folded out of the program (PD_FOLD_NEG), bit 31
     int hoist = 0;         // PD_HOIST: the first opcode after the program's hoisted prefix, or 0
     bool hy = false;       // ... a prefix of y alone
+    int h_at = 0, h_to = 0;   // PD_HOIST_SUB: the hoisted segment's span, its kind, first word
+    bool h_y = false;
+    uint32_t h_w0 = 0u;
     if (!slow) {
         const uint32_t dh = rd_word(a.dec + beg);
         slow = (dh & 0xffu) != 0u || (int)((dh >> 8) & 0xffu) > MAXD;
         u_sgn = (dh & 0x10000u) << 15;
+        if (!CX && hoist_sub<PROB>() && a.hseg && !slow) {
+            // (the decoder rewrote the segment's first opcode: every part of a split launch
+            // evaluates it -- the same values into the same slot)
+            const int32_t* hs = a.hseg + 4 * cand;
+            h_at = __builtin_amdgcn_readfirstlane(hs[1]);
+            if (h_at) {
+                h_w0 = (uint32_t)__builtin_amdgcn_readfirstlane(hs[0]);
+                h_to = __builtin_amdgcn_readfirstlane(hs[2]);
+                h_y = __builtin_amdgcn_readfirstlane(hs[3]) != 0;
+            }
+        }
         if (!CX && PD_HOIST && a.hoist && parts == 1) {
             hoist = (int)((dh >> 17) & 0x3fffu);
             hy = (dh >> 31) != 0u;
@@ -943,9 +1046,10 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     // non-finite coefficient (0 * inf = NaN in the others) the candidate is not hoisted.
     // (a.nx <= 64, checked by the host, which passes a.hoist = NULL otherwise)
     if constexpr (!CX && PD_HOIST) {
-        if (hoist)
-            hoist = hoist_prefix<K, MAXD>(a.dec + beg, hoist, PROB != PDEVAL_PROBLEM_FORCE_FREE && hy, a.gx, a.nx, a.ny, a.ptab,
-                                          a.hoist + (size_t)cand * (K + 1) * 64, lane, stk, y0, inv_y0);
+        if (hoist || h_at)
+            hoist_parts<K, MAXD, hoist_sub<PROB>()>(a.dec + beg, hoist, PROB != PDEVAL_PROBLEM_FORCE_FREE && hy, h_at, h_to, h_w0, h_y,
+                                 a.gx, a.nx, a.ny, a.ptab, a.hoist + (size_t)cand * hoist_stride(K),
+                                 a.hoist + (size_t)cand * hoist_stride(K) + (K + 1) * 64, lane, stk, y0, inv_y0);
     }
     GridMax<PROB != PDEVAL_PROBLEM_FORCE_FREE> gm;   // (PD_DIVFREE) the lane's running maximum of q
     double qmax = 0.0;
@@ -1005,7 +1109,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             if constexpr (!kv_late) load_kv();
             J u[W];
             if (!CX && PD_HOIST && hoist) {
-                const double* hb = a.hoist + (size_t)cand * (K + 1) * 64;
+                const double* hb = a.hoist + (size_t)cand * hoist_stride(K);
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
 #pragma unroll
@@ -1019,7 +1123,8 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                     }
                 }
             }
-            L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane, pt, hoist ? hoist : 1);
+            L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane, pt, hoist ? hoist : 1, 0,
+                   h_at ? a.hoist + (size_t)cand * hoist_stride(K) + (K + 1) * 64 : nullptr, row, a.nx - 1, h_y);
             if constexpr (kv_late) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {

@@ -81,6 +81,8 @@ struct KernelArgs {
     int32_t* dec;               // n_words: the programs pre-decoded for the lean grid passes
     uint64_t* fmask;            // lean passes: per candidate and 64-point grid chunk, the lanes
                                 // that failed the tier-1 test (what tier 2 re-checks); NULL = none
+    int32_t* hseg;              // decoder: per candidate {original word, start, end, y?} of its
+                                // hoisted segment (start 0: none; pdeval_grid.h PD_HOIST_SUB)
     double* hoist;              // lean passes: per candidate, the pure-x coefficients of its
                                 // x-only prefix at every grid row, [cand][k][row] (pdeval_grid.h
                                 // PD_HOIST); NULL = not hoisted
@@ -147,6 +149,10 @@ struct T2Acc {
     uint32_t grad;
     int32_t done;                   // parts merged so far
 };
+
+// doubles per candidate of the hoist buffer (pdeval_grid.h PD_HOIST): the prefix's K + 1 pure
+// coefficients and the segment's nc(K) coefficients, 64 rows (or lanes) each
+PD_HD constexpr size_t hoist_stride(int K) { return (size_t)(K + 1 + (K + 1) * (K + 2) / 2) * 64; }
 
 // Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).
 enum : uint32_t {

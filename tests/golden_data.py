@@ -142,7 +142,7 @@ FF_COUNT_SLACK = {
 # long enough for the reference to expand it (validator.py:407-426, "expanded det != 0") while
 # SymPy leaves the sqrt(rho/z) terms un-merged -- are reproduced by the 'replay' mode
 # (pdeval/symbolic.py); the default mode gives the true verdict.
-FF_D5 = ('ff_d5_s400.jsonl', 'ff_d5_s4000_t20.jsonl', 'ff_d5_s7000_t20.jsonl')
+FF_D5 = ('ff_d5_s400.jsonl', 'ff_d5_s4000_t20.jsonl', 'ff_d5_s7000_t20.jsonl', 'ff_d5_s7600_t20.jsonl')
 FF_D5_SYMBOLIC_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))'}
 # Every decided force-free fixture row on which the default mode ('off': the grid's det == 0
 # and the structural rules) and the reference's verdict differ -- all decided in the reference's
@@ -154,7 +154,8 @@ FF_OFF_MODE_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))', 'sqrt(square(inv(rho))
                           # ... and squares under a fractional power that the NONSMOOTH2D rule
                           # rejects but SymPy's Abs form lets the reference prove
                           'pow_neg_3_2(square(rho - z))', 'pow_neg_3_2(square(rho**2 + z**2 - z - 1))',
-                          'pow_3_2(square(-z + neg(rho)))'}
+                          'pow_3_2(square(-z + neg(rho)))',
+                          'sqrt(square(rho**2 + z**2 - 1/(rho**2 + z**2)))'}   # (d5 s7600)
 # depth-5 point rejects whose reference text carries a number SymPy's cancel/simplify made up:
 # det_M.subs(p*).evalf(50) -- the exact value, what the device and the oracle print -- against
 # the reference's cancel(together(.)) -> simplify -> evalf pipeline (validator.py:366-394).

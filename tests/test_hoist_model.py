@@ -31,12 +31,26 @@ def _flops(pd_, s):
     ('force_free', 'exp(z)*rho', False),         # a prefix of z alone: hoisted for Kerr only
     ('kerr_magnetosphere', 'exp(x)*r', True),    # Kerr's lane coordinate x: once per lane
     ('kerr_magnetosphere', 'sqrt(r + 1)*x', True),
+    # a segment of one coordinate as a right operand (PD_HOIST_SUB: Kerr only)
+    ('kerr_magnetosphere', 'exp(r*x) + sqrt(x + 1)', True),
+    ('force_free', 'exp(rho*z) + sqrt(z + 3)', False),
 ])
 def test_prefix_rule(prob, s, hoisted):
     pd_ = P.get(prob)
     total, pre = _flops(pd_, s)
     assert (pre > 0) is hoisted, (s, total, pre)
     assert 0 <= pre < total - (2 * 160 if pd_.problem_id == 0 else 16)
+
+
+def test_kerr_segment_and_prefix_add():
+    """Kerr hoists a prefix and a later segment of one coordinate together (the segment after
+    the prefix's end): exp(r) * x + log(x + 2) -- the prefix PUSH_X EXP and the segment
+    log(x + 2) -- counts both."""
+    pd_ = P.get('kerr_magnetosphere')
+    _, both = _flops(pd_, 'exp(r) * x + log(x + 2)')
+    _, pre = _flops(pd_, 'exp(r) * x')
+    _, seg = _flops(pd_, 'r * x + log(x + 2)')
+    assert pre > 0 and seg > 0 and both == pytest.approx(pre + seg)
 
 
 def test_d4_workload_share():
