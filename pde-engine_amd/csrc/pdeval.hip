@@ -782,7 +782,7 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     c->d_hseg = nullptr;
     if (c->hoist) {
         // per candidate: the prefix's pure coefficients (K + 1 rows of 64) and the segment's
-        // whole jet (nc(K) rows of 64) -- pd::hoist_stride
+        // whole jet (nc(K) rows of 64, Kerr only) -- pd::hoist_stride
         const int K = c->problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
         HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)cap * pd::hoist_stride(K) * sizeof(double)));
         HIPCHK(c, hipMalloc(&c->d_hseg, (size_t)cap * 4 * sizeof(int32_t)));

@@ -151,8 +151,9 @@ struct T2Acc {
 };
 
 // doubles per candidate of the hoist buffer (pdeval_grid.h PD_HOIST): the prefix's K + 1 pure
-// coefficients and the segment's nc(K) coefficients, 64 rows (or lanes) each
-PD_HD constexpr size_t hoist_stride(int K) { return (size_t)(K + 1 + (K + 1) * (K + 2) / 2) * 64; }
+// coefficients and, Kerr (K = 2) only, the segment's nc(K) coefficients, 64 rows (or lanes) each
+// (force-free hoists no segments: 2.5 KiB per candidate instead of 10)
+PD_HD constexpr size_t hoist_stride(int K) { return (size_t)(K + 1 + (K == 4 ? 0 : (K + 1) * (K + 2) / 2)) * 64; }
 
 // Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).
 enum : uint32_t {
