@@ -122,6 +122,7 @@ struct pdeval_ctx {
     // the lean passes' failing lanes per candidate and grid chunk, cap x chunks words, which
     // tier 2 re-checks instead of the whole grid (env PDEVAL_TIER2_MASK=0: none, A/B)
     bool tier2_mask = true;
+    int deep_parts = PD_DEEP_PARTS;     // the stack-8 lists' waves per candidate (env PDEVAL_DEEP_PARTS)
     uint64_t* d_fmask = nullptr;
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
     double* d_noise = nullptr;      // fp64 noise bounds at the reference points, cap * 4
@@ -444,6 +445,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_HOIST")) c->hoist = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_HOIST_SUB")) c->hoist_sub = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_TIER2_MASK")) c->tier2_mask = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_DEEP_PARTS")) c->deep_parts = atoi(v) > 1 ? PD_DEEP_PARTS : 1;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     if ((e = hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking)) != hipSuccess)
@@ -1037,9 +1039,16 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // pass 3: stack 4..8 (rare; the flattener guarantees <= PDEVAL_MAX_STACK)
     mark(4);
     if (dmax > 3) {
-        hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
-                           dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
-                           (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
+        // (the stack-8 list: a few dozen to a few hundred candidates, each grid split over
+        // PD_DEEP_PARTS waves -- pdeval_kernels.h validate_kernel; env PDEVAL_DEEP_PARTS=1: one wave)
+        if (c->deep_parts > 1)
+            hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true, PD_DEEP_PARTS>),
+                               dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
+                               (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
+        else
+            hipLaunchKernelGGL((validate_kernel<PROB, double, PDEVAL_MAX_STACK, true>),
+                               dim3((unsigned)std::min<int64_t>(4 * blocks, 1024)), dim3(64),
+                               (stack_lds<double, K, PDEVAL_MAX_STACK>(1)), s, follow(L_DEFER2, -1, L_ESC));
         HIPCHK(c, hipGetLastError());
     }
     if constexpr (FF) {
@@ -1063,9 +1072,14 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
         HIPCHK(c, hipGetLastError());
         mark(6);
         if (dmax > 2) {
-            hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),
-                               dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
-                               (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
+            if (c->deep_parts > 1)
+                hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true, PD_DEEP_PARTS>),
+                                   dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
+                                   (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
+            else
+                hipLaunchKernelGGL((validate_kernel<PROB, cplx, PDEVAL_MAX_STACK, true>),
+                                   dim3((unsigned)std::min<int64_t>(4 * blocks, 512)), dim3(64),
+                                   (stack_lds<cplx, K, PDEVAL_MAX_STACK>(1)), s, follow(L_CPLX_DEEP, -1, L_ESC_C));
             HIPCHK(c, hipGetLastError());
         }
     } else {

@@ -1215,8 +1215,17 @@ template <class T, int K, int MAXD> struct Interp {
 };
 
 // ------------------------------------------------------------------ the kernel
+#ifndef PD_DEEP_PARTS
+#define PD_DEEP_PARTS 16
+#endif
 // PROB: PDEVAL_PROBLEM_FORCE_FREE (K = 4) or PDEVAL_PROBLEM_KERR (K = 2).
-template <int PROB, class T, int MAXD, bool PERSISTENT>
+// PARTS > 1 (the persistent deep-list passes): a candidate whose point stage pass 0 decided has
+// its grid chunks split over PARTS waves (contiguous ranges); each part adds its counts into the
+// list entry's accumulator (a.t2acc, zero between launches) and the part that completes the
+// entry writes the outputs -- the stack-8 lists hold a few dozen to a few hundred candidates, and
+// one wave each left the chip idle (Kerr pass 3: 2.95 ms for 98 candidates).  Sums, maxima and
+// ORs do not depend on the split.  Any other candidate is taken by part 0 alone.
+template <int PROB, class T, int MAXD, bool PERSISTENT, int PARTS = 1>
 #ifndef PD_WAVES_PER_SIMD
 #define PD_WAVES_PER_SIMD 4
 #endif
@@ -1248,7 +1257,9 @@ void validate_kernel(KernelArgs a) {
     int64_t nwork = a.list_count ? (int64_t)(*a.list_count) : (a.list ? a.list_cap : a.n);
     if (a.list && nwork > a.list_capacity) nwork = a.list_capacity;
 
-    for (int64_t wi = wave0; wi < nwork; wi = PERSISTENT ? wi + wstride : nwork) {
+    for (int64_t wp = wave0; wp < nwork * PARTS; wp = PERSISTENT ? wp + wstride : nwork * PARTS) {
+        const int64_t wi = wp / PARTS;
+        const int part = (int)(wp - wi * PARTS);
         const int64_t cand = a.list ? checked_cand(a, (int64_t)__builtin_amdgcn_readfirstlane((int)a.list[wi]), ERRW_GENERIC) : wi;
         if (cand < 0) continue;
         int64_t beg = a.offsets[cand], end = a.offsets[cand + 1];
@@ -1292,6 +1303,9 @@ void validate_kernel(KernelArgs a) {
             }
             status = PDEVAL_CLS_UNSUPPORTED;  // deeper than the last variant takes
         }
+        // split over the parts only a grid whose point stage is decided (no chunk 0)
+        const bool split = PARTS > 1 && p0 && status < 0 && a.t2acc;
+        if (PARTS > 1 && !split && part != 0) continue;
         double q_ref = 0.0;        // FF: q*, Kerr: max |lhs| over reference points
         bool point_reject = (ps & 3) == P0_REJECT;
         bool point_final = p0;     // non-finite at a reference point, or decided by pass 0: no tier 2
@@ -1303,7 +1317,13 @@ void validate_kernel(KernelArgs a) {
         const int per_row = a.ny >> 6;
         const int nchunks = 1 + a.nx * per_row;
         const double y_lane = a.gy[lane];  // row slice 0; other slices reload below
-        for (int ch = p0 ? 1 : 0; ch < nchunks && status < 0; ++ch) {
+        int ch_beg = p0 ? 1 : 0, ch_end = nchunks;
+        if (split) {
+            const int ng = nchunks - 1;
+            ch_beg = 1 + (int)((int64_t)ng * part / PARTS);
+            ch_end = 1 + (int)((int64_t)ng * (part + 1) / PARTS);
+        }
+        for (int ch = ch_beg; ch < ch_end && status < 0; ++ch) {
             bool active;
             int p;               // point index: reference points first, then the grid row-major
             double x, y;
@@ -1386,7 +1406,44 @@ void validate_kernel(KernelArgs a) {
         }
         // wave reductions
         qmax = wave_max(qmax);
-        const bool any_grad = __any(grad_nz) && !(ps & P0_CONST);
+        bool grad_w = __any(grad_nz);
+        if (split) {
+            // merge this part into the entry's accumulator; the last part carries on (a status
+            // from the interpreter -- malformed, unsupported -- travels as bits of `grad`)
+            int last = 0;
+            if (lane == 0) {
+                T2Acc* A = a.t2acc + wi;
+                atomicAdd(&A->nb1, nbad);
+                atomicAdd(&A->nfin, nfin);
+                atomicAdd(&A->nnonfin, nnonfin);
+                atomicMax(&A->qmax_bits, (unsigned long long)__double_as_longlong(qmax));   // qmax >= 0
+                const uint32_t g = (grad_w ? 1u : 0u) | (status == PDEVAL_CLS_BAD_PROGRAM ? 2u : 0u) |
+                                   (status == PDEVAL_CLS_UNSUPPORTED ? 4u : 0u);
+                if (g) atomicOr(&A->grad, g);
+                __threadfence();
+                if (atomicAdd(&A->done, 1) == PARTS - 1) {
+                    __threadfence();
+                    nbad = atomicAdd(&A->nb1, 0);
+                    nfin = atomicAdd(&A->nfin, 0);
+                    nnonfin = atomicAdd(&A->nnonfin, 0);
+                    qmax = __longlong_as_double((long long)atomicMax(&A->qmax_bits, 0ull));
+                    const uint32_t gm = atomicOr(&A->grad, 0u);
+                    grad_w = (gm & 1u) != 0u;
+                    status = (gm & 2u) ? PDEVAL_CLS_BAD_PROGRAM : (gm & 4u) ? PDEVAL_CLS_UNSUPPORTED : -1;
+                    A->nb1 = A->nb2 = A->nfin = A->nnonfin = A->done = 0;   // ready for the next use
+                    A->grad = 0u;
+                    A->qmax_bits = 0ull;
+                    last = 1;
+                }
+            }
+            if (!__builtin_amdgcn_readfirstlane(last)) continue;   // lane 0 is the first active lane
+            status = __builtin_amdgcn_readfirstlane(status);
+            nbad = __builtin_amdgcn_readfirstlane(nbad);
+            nfin = __builtin_amdgcn_readfirstlane(nfin);
+            nnonfin = __builtin_amdgcn_readfirstlane(nnonfin);
+            grad_w = __builtin_amdgcn_readfirstlane((int)grad_w) != 0;
+        }
+        const bool any_grad = grad_w && !(ps & P0_CONST);
         if (lane == 0) {
             int cls = status;
             if (cls < 0) {

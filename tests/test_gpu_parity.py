@@ -629,3 +629,18 @@ def test_tier2_masked_equals_full(pid, data, n):
         if k in on:
             assert np.array_equal(on[k], off_[k], equal_nan=on[k].dtype.kind == 'f'), \
                 (k, np.flatnonzero(np.any((on[k] != off_[k]).reshape(len(on[k]), -1), axis=1))[:10])
+
+
+@pytest.mark.parametrize('pid, data', [(0, 'force_free_d4_validated.npz'), (1, 'kerr_magnetosphere_d4_stream.npz')])
+def test_deep_lists_split_equals_single_wave(pid, data):
+    """The stack-8 lists' generic kernel with each grid split over PD_DEEP_PARTS waves (counts
+    merged in the list entry's accumulator) gives every output of the single-wave kernel, on the
+    force-free d4 workload (its complex stack-8 list) and the whole Kerr d4 stream (its pass 3)."""
+    d = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'data', data))
+    ops, off = d['ops'], d['offsets']
+    split = _validate_env(pid, ops, off, {'PDEVAL_DEEP_PARTS': '16'})
+    single = _validate_env(pid, ops, off, {'PDEVAL_DEEP_PARTS': '1'})
+    for k in ('status', 'verdict', 'n_bad', 'n_nonfinite', 'q_grid', 'q_ref', 'res_ref', 'fingerprint'):
+        if k in split:
+            assert np.array_equal(split[k], single[k], equal_nan=split[k].dtype.kind == 'f'), \
+                (k, np.flatnonzero(np.any((split[k] != single[k]).reshape(len(split[k]), -1), axis=1))[:10])
