@@ -132,7 +132,7 @@ __device__ __forceinline__ bool neg_fold_ok(const int32_t* prog, int plen) {
     return true;
 }
 
-// ---- x-only prefixes (PD_HOIST).  A program whose first opcodes compute a value of x alone
+// ---- single-coordinate prefixes (PD_HOIST).  A program whose first opcodes compute a value of x alone
 // (u = exp(rho) * z: PUSH_X EXP | PUSH_Y MUL) computes the same jet at every lane of a grid row:
 // the lean passes evaluate that prefix once per candidate for all rows at once (one row per
 // lane), keep the jets in a per-candidate buffer and start every row's run after it.  A prefix
@@ -181,8 +181,8 @@ __global__ __launch_bounds__(256) void decode_kernel(KernelArgs a) {
     int pc = 1, d = 0, dmax = 0, last = -1;
     int sg[5] = {1, 1, 1, 1, 1};   // PD_FOLD_NEG: sign of the value at each stack depth (1-based)
     // PD_HOIST: which coordinates the value at each stack depth depends on (bit 0 x, bit 1 y,
-    // bit 2 the imaginary unit), and the longest x-only prefix of the program that ends at
-    // depth 1 (its last visited opcode, and whether it holds a heavy opcode)
+    // bit 2 the imaginary unit), and the longest prefix of one coordinate that ends at depth 1
+    // (its last visited opcode, whether it holds a heavy opcode, whether it is of y)
     uint32_t msk[5] = {0u, 0u, 0u, 0u, 0u};
     int hoist_last = -1;
     bool hoist_alive = true, heavy = false, hoist_heavy = false, hoist_y = false;

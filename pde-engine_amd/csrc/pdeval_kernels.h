@@ -83,10 +83,10 @@ struct KernelArgs {
                                 // that failed the tier-1 test (what tier 2 re-checks); NULL = none
     int32_t* hseg;              // decoder: per candidate {original word, start, end, y?} of its
                                 // hoisted segment (start 0: none; pdeval_grid.h PD_HOIST_SUB)
-    double* hoist;              // lean passes: per candidate, the pure-x coefficients of its
-                                // x-only prefix at every grid row, [cand][k][row] (pdeval_grid.h
-                                // PD_HOIST); NULL = not hoisted
-                                // (pdeval_grid.h decode_kernel), or NULL
+    double* hoist;              // lean passes: per candidate (hoist_stride doubles), the pure
+                                // coefficients of its hoisted prefix at every grid row or lane
+                                // and, Kerr, its hoisted segment's jets (pdeval_grid.h PD_HOIST);
+                                // NULL = nothing hoisted
     // the problem's constants per stage (PDEVAL_IMM_PRM; Kerr M, a): point stage (fp64 and
     // double-double) and the constant test / grid stage
     PrmTab<double> prm_pt, prm_grid;
