@@ -59,10 +59,18 @@ def load_workload(problem):
     raise FileNotFoundError(f'data/{problem}_d*_*.npz missing')
 
 
-def pmc_traffic(n_per_launch, dominant=DOMINANT):
+def _pmc_pass1(k, n_cand, n_batch):
+    """Pass-1 candidates of the profiled launch: recorded by scripts/pmc_summary.py from the
+    profiled run's own bench line, or (older summaries) its launched waves scaled by this
+    batch's pass-1 share -- the same workload, tiled and shuffled the same way."""
+    return k.get('pass1_candidates') or k['candidates'] * (n_cand / max(1, n_batch))
+
+
+def pmc_traffic(n_per_launch, dominant=DOMINANT, n_batch=None):
     """HBM bytes per launch of the dominant kernel from the newest committed PMC summary
     (profiles/*_pmc.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc
-    passes), scaled to this launch's candidate count; None if there is none."""
+    passes), per pass-1 candidate of the profiled launch, scaled to this launch's pass-1
+    candidates; None if there is none."""
     files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))
     for path in reversed(files):          # the newest summary (by name) that has the kernel
         with open(path) as f:
@@ -71,7 +79,8 @@ def pmc_traffic(n_per_launch, dominant=DOMINANT):
         # summaries from before the ROT instances name the kernel without its third argument
         k = kern.get(dominant) or kern.get(dominant.replace(', false, false>', ', false>'))
         if k and k.get('candidates') and 'hbm_bytes_per_launch' in k:
-            return k['hbm_bytes_per_launch'] / k['candidates'] * n_per_launch, os.path.basename(path)
+            per = k['hbm_bytes_per_launch'] / _pmc_pass1(k, n_per_launch, n_batch or n_per_launch)
+            return per * n_per_launch, os.path.basename(path)
     return None, None
 
 
@@ -369,6 +378,9 @@ class ProblemBench:
             dist.barrier()
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
+        # the last step's device error word (pdeval_device_error: a work-list entry outside the
+        # batch would have been skipped silently): raises if it is set
+        self.ctx.device_error()
         kern = float(np.mean([s.elapsed_time(e) for s, e in ev]))
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         if self.world > 1:
@@ -435,14 +447,20 @@ class ProblemBench:
         p1_flops = float(fl[in_p1].sum()) - rerouted * float(fl[in_p1].mean() if in_p1.any() else 0.0)
         p1_ms = pass_ms['pass1_stack2']
         achieved_tf = p1_flops / (p1_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic(int(in_p1.sum()), self.dominant)
+        n_p1 = int(in_p1.sum()) - rerouted
+        traffic, traffic_src = pmc_traffic(n_p1, self.dominant, self.n)
         roof = {'bound': 'valu_fp64', 'kernel': self.dominant, 'achieved': achieved_tf,
                 'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved_tf / FP64_PEAK_TFLOPS,
                 'traffic': traffic, 'traffic_source': traffic_src,
-                'kernel_ms': p1_ms, 'kernel_candidates': int(in_p1.sum()) - rerouted,
+                'kernel_ms': p1_ms, 'kernel_candidates': n_p1,
                 'flops_per_launch': p1_flops,
                 'flops_model': 'hoisted prefixes once per row' if self.hoist else 'every opcode at every point'}
-        roof.update(pmc_flop_frac(self.dominant, int(in_p1.sum()) - rerouted, p1_ms))
+        roof['traffic_per_candidate'] = traffic / n_p1 if traffic else None
+        roof.update(pmc_flop_frac(self.dominant, n_p1, p1_ms, self.n))
+        if roof.get('counter_flops_per_candidate'):
+            # the FLOP model against the executed FP64 operations
+            roof['model_flops_per_candidate'] = p1_flops / max(1, n_p1)
+            roof['model_over_counters'] = roof['model_flops_per_candidate'] / roof['counter_flops_per_candidate']
         return {'roofline': roof, 'pass_ms': {k: round(v, 3) for k, v in pass_ms.items()}, 'counts': counts}
 
     def roofline_hbm(self, kern_ms) -> dict:
@@ -486,11 +504,13 @@ def kerr_subrecord(n, steps, warmup, world, rank, local, dev):
         kb.close()
 
 
-def pmc_flop_frac(dominant, n_cand, kernel_ms):
+def pmc_flop_frac(dominant, n_cand, kernel_ms, n_batch):
     """The dominant kernel's FP64 FLOP rate from the hardware counters (the newest committed
-    PMC summary with SQ FP64 counts: (2 FMA + MUL + ADD) x 64 lanes per wave = per candidate,
-    scaled to this launch's candidates and its event time), beside the FLOP model's fraction;
-    {} when no summary has them.  (TRANS -- rcp, sqrt estimates -- is not counted as FLOPs.)"""
+    PMC summary with SQ FP64 counts: (2 FMA + MUL + ADD) x 64 lanes, per launch, divided by the
+    pass-1 candidates of the profiled launch -- not by its launched waves, which include the
+    candidates pass 1 hands on -- then scaled to this launch's pass-1 candidates and its event
+    time), beside the FLOP model's fraction; {} when no summary has them.  (TRANS -- rcp, sqrt
+    estimates -- is not counted as FLOPs.)"""
     files = sorted(glob.glob(os.path.join(ROOT, 'profiles', '*_pmc.json')))
     for path in reversed(files):
         with open(path) as f:
@@ -499,7 +519,7 @@ def pmc_flop_frac(dominant, n_cand, kernel_ms):
         if k and k.get('candidates') and 'SQ_INSTS_VALU_FMA_F64' in k:
             fl = 64.0 * (2 * k['SQ_INSTS_VALU_FMA_F64'] + k.get('SQ_INSTS_VALU_MUL_F64', 0.0) +
                          k.get('SQ_INSTS_VALU_ADD_F64', 0.0))
-            per = fl / k['candidates']
+            per = fl / _pmc_pass1(k, n_cand, n_batch)
             tf = per * n_cand / (kernel_ms * 1e-3) / 1e12
             return {'counter_flops_per_candidate': per, 'counter_achieved': tf,
                     'counter_frac': tf / FP64_PEAK_TFLOPS, 'counter_source': os.path.basename(path)}

@@ -1149,6 +1149,8 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     return PDEVAL_OK;
 }
 
+static int check_errw(pdeval_ctx* c, uint32_t w, const char* path, int64_t n, int captured);
+
 static int validate_device(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, const int64_t* d_offsets,
                            int64_t n, const pdeval_params* params, const pdeval_outputs* d_out, void* stream,
                            int zero_bits, int dmax) {
@@ -1184,6 +1186,15 @@ extern "C" int pdeval_validate_device(pdeval_ctx* c, const int32_t* d_ops, int64
                                       const pdeval_outputs* d_out, void* stream, int zero_bits) {
     // device-resident programs: their depths are not known here, every pass is launched
     return validate_device(c, d_ops, n_words, d_offsets, n, params, d_out, stream, zero_bits, PDEVAL_MAX_STACK);
+}
+
+extern "C" int pdeval_device_error(pdeval_ctx* c, uint32_t* word) {
+    if (!c || !word) return PDEVAL_ERR_ARG;
+    *word = 0u;
+    if (!c->d_counts) return PDEVAL_OK;   // no call yet
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpy(word, c->d_counts + PD_N_LISTS, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return check_errw(c, *word, "device", -1, -1);
 }
 
 // ---- small host batches (the plugin's one-candidate validate(), the inline driver loop

@@ -27,7 +27,7 @@ EXPORTS = (
     'pdeval_compile_batch', 'pdeval_canonical', 'pdeval_point_eval', 'pdeval_point_states',
     'pdeval_comm_unique_id', 'pdeval_comm_init', 'pdeval_gather_bits', 'pdeval_comm_destroy',
     'pdeval_default_kerr_constants', 'pdeval_set_kerr_constants', 'pdeval_compile_batch_mt',
-    'pdeval_format_reasons',
+    'pdeval_format_reasons', 'pdeval_device_error',
 )
 MAX_BATCH = 1 << 30          # PDEVAL_MAX_BATCH
 UNIQUE_ID_BYTES = 128
@@ -91,6 +91,7 @@ def load(path: Optional[str] = None) -> C.CDLL:
     lib.pdeval_validate_batch.argtypes = [vp, vp, i64, vp, i64, C.POINTER(Params), C.POINTER(Outputs)]
     lib.pdeval_validate_device.argtypes = [vp, vp, i64, vp, i64, C.POINTER(Params),
                                            C.POINTER(Outputs), vp, C.c_int]
+    lib.pdeval_device_error.argtypes = [vp, C.POINTER(C.c_uint32)]
     lib.pdeval_program_depth.argtypes = [vp, i64]
     lib.pdeval_program_flops.argtypes = [C.c_int, vp, i64]
     lib.pdeval_program_flops.restype = dbl
@@ -277,6 +278,14 @@ class Context:
         rc = self.lib.pdeval_validate_device(self.h, d_ops, n_words, d_offsets, n, C.byref(prm),
                                              C.byref(d_out), stream, int(zero_bits))
         _check(self.h, rc)
+
+    def device_error(self) -> int:
+        """The device error word of the most recent validate_device call (call after its stream
+        is synchronized): 0, or PdevalError naming the kernel families whose work-list check met
+        an entry outside the batch (pdeval_device_error)."""
+        w = C.c_uint32(0)
+        _check(self.h, self.lib.pdeval_device_error(self.h, C.byref(w)))
+        return int(w.value)
 
 
 def comm_unique_id() -> bytes:

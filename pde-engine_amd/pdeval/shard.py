@@ -136,31 +136,48 @@ def gather_verdicts_native(ctx, local_bits, ranges: Sequence[Tuple[int, int]], s
 
 
 def final_verdicts(pd, kerr, params, n_grid: int, items, r: dict, ops, off, keys=None,
-                   symbolic: str = 'off') -> np.ndarray:
+                   symbolic: str = 'off', symbolic_timeout: Optional[float] = None,
+                   omega: str = '0') -> np.ndarray:
     """This rank's final (plugin) verdicts: the device outputs ``r`` of its shard (host
     arrays) through ``pdeval.batch.apply_host_steps``; returns bool[n] (``r`` is updated in
-    place: ``status``, ``verdict``).
+    place: ``status``, ``verdict``, and the host steps' non-array entries -- the strict mode's
+    ``reason_override`` and ``strict`` statistics).  ``omega`` and ``symbolic_timeout`` are the
+    plugin's (``BatchValidator.omega`` / ``.symbolic_timeout``): the symbolic replay runs the
+    reference's stage at the same Omega the device used.
 
     ``keys`` (optional, int[n]): a program id per candidate when the shard repeats programs (the
     bench's tiled batch).  The host steps then run once per distinct program, on its first
     occurrence, and the resulting class is given to every occurrence -- the device's outputs
     are a function of the program alone (bench.py checks that duplicates agree)."""
-    from .batch import apply_host_steps
+    from .batch import SYMBOLIC_TIMEOUT_S, apply_host_steps
     from .opcodes import CLS_ACCEPT
+    tmo = SYMBOLIC_TIMEOUT_S if symbolic_timeout is None else symbolic_timeout
     st = np.asarray(r['status'])
     n = len(st)
     if 'verdict' not in r:
         r['verdict'] = st == CLS_ACCEPT
     if keys is None:
-        apply_host_steps(pd, kerr, params, n_grid, items, r, ops, off, symbolic)
+        apply_host_steps(pd, kerr, params, n_grid, items, r, ops, off, symbolic, tmo, omega)
         return np.asarray(r['verdict'], dtype=bool).copy()
     keys = np.asarray(keys)
     _, first, inv = np.unique(keys, return_index=True, return_inverse=True)
     sub = {k: np.asarray(v)[first] for k, v in r.items() if isinstance(v, np.ndarray) and len(v) == n}
     sub_ops, sub_off = _gather(ops, off, first)
-    apply_host_steps(pd, kerr, params, n_grid, [items[i] for i in first], sub, sub_ops, sub_off, symbolic)
+    apply_host_steps(pd, kerr, params, n_grid, [items[i] for i in first], sub, sub_ops, sub_off, symbolic,
+                     tmo, omega)
     st[:] = sub['status'][inv]
     r['verdict'] = st == CLS_ACCEPT
+    # the host steps' per-candidate extras, mapped back to every occurrence: the row-keyed dicts
+    # (reason_override, Kerr evidence; keyed by position in the distinct-program list) and the
+    # strict mode's statistics
+    for k, v in sub.items():
+        if k in ('status', 'verdict') or (isinstance(v, np.ndarray) and len(v) == len(first)):
+            continue
+        if isinstance(v, dict) and k in ('reason_override', 'evidence'):
+            rows = np.nonzero(np.isin(inv, np.fromiter(v.keys(), dtype=np.int64)))[0] if v else []
+            r[k] = {int(j): v[int(inv[j])] for j in rows}
+        else:
+            r[k] = v
     return np.asarray(r['verdict'], dtype=bool).copy()
 
 

@@ -29,8 +29,29 @@ def load(pass_dir):
     return agg, disp
 
 
+def pass1_candidates(src):
+    """The candidates pass 1 actually evaluated in the profiled bench run (its JSON line's
+    roofline.kernel_candidates), per dominant kernel: the divisor of the per-candidate counter
+    values -- SQ_WAVES counts every launched wave, and the candidates pass 1 does not take
+    (deeper stacks, complex at p*) leave after a few instructions."""
+    got = {}
+    for f in glob.glob(os.path.join(src, '*.log')):
+        for line in open(f, errors='replace'):
+            if not line.startswith('{'):
+                continue
+            try:
+                r = json.loads(line)
+            except ValueError:
+                continue
+            roof = r.get('roofline') or {}
+            if roof.get('kernel') and roof.get('kernel_candidates'):
+                got[roof['kernel']] = roof['kernel_candidates']
+    return got
+
+
 def main():
     src, out = sys.argv[1], sys.argv[2]
+    p1 = pass1_candidates(src)
     kern = collections.defaultdict(dict)
     for p in sorted(os.listdir(src)):
         d = os.path.join(src, p)
@@ -45,7 +66,9 @@ def main():
     res = {}
     for k, v in kern.items():
         r = dict(v)
-        r['candidates'] = v.get('SQ_WAVES')
+        r['candidates'] = v.get('SQ_WAVES')           # every launched wave (one per candidate)
+        if k in p1:
+            r['pass1_candidates'] = p1[k]              # the ones pass 1 evaluated
         if 'FETCH_SIZE' in v and 'WRITE_SIZE' in v:
             r['hbm_bytes_per_launch'] = 2 * v['FETCH_SIZE'] * 1024 + v['WRITE_SIZE'] * 1024
         res[k] = r

@@ -361,6 +361,7 @@ def test_validate_device_limits_and_bad_programs(ff_ctx):
     ff_ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out,
                            stream=stream.cuda_stream)
     torch.cuda.synchronize(dev)
+    assert ff_ctx.device_error() == 0
     st = outs['status'].cpu().numpy()
     assert st.tolist() == [1, 0, 5, 6], st           # reject, accept, UNSUPPORTED, BAD_PROGRAM
     bits = np.unpackbits(outs['verdict_bits'].cpu().numpy(), bitorder='little')[:n]
@@ -398,6 +399,7 @@ def test_sharded_chain_world1_native_and_torch_gather():
         torch.cuda.synchronize(dev)
         ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out, stream=stream.cuda_stream)
         torch.cuda.synchronize(dev)
+        assert ctx.device_error() == 0
         via_torch = gather_verdicts(bits.cpu(), ranges)
         init_native_comm(ctx, 0, 1)
         via_rccl = gather_verdicts_native(ctx, bits, ranges)

@@ -184,6 +184,7 @@ def _device_outputs(ctx, o, f, n_ref):
     torch.cuda.synchronize(dev)
     ctx.validate_device(d_ops.data_ptr(), d_ops.numel(), d_off.data_ptr(), n, d_out, stream=stream.cuda_stream)
     torch.cuda.synchronize(dev)
+    assert ctx.device_error() == 0
     r = {k: v.cpu().numpy() for k, v in outs.items()}
     r['verdict'] = np.unpackbits(r.pop('verdict_bits'), bitorder='little')[:n].astype(bool)
     return r
@@ -222,6 +223,43 @@ def test_small_batch_graph_path_equals_direct():
                 x = np.asarray(a[k])
                 assert np.array_equal(x, np.asarray(b[k]), equal_nan=x.dtype.kind == 'f'), (n, k)
                 assert np.array_equal(x.ravel(), full[k].ravel(), equal_nan=x.dtype.kind == 'f'), (n, k, 'device')
+    finally:
+        g.close()
+        d.close()
+
+
+def test_graph_replay_after_large_batches():
+    """The round-5 fault's sequence (DESIGN.md §3 "Robustness of the launch chain"): a small
+    batch captures its graph, a large direct batch (and a large device-entry batch) leaves the
+    list counters high, then the SAME small graph is replayed.  Every replay must start from
+    zeroed counters: the device error word stays 0 and the outputs equal a PDEVAL_GRAPH=0
+    context's, call after call."""
+    from pdeval import problem_defs as P
+    from pdeval.workload import gather_programs
+    pd_ = P.force_free()
+    strs = [r['expr'] for r in G.decided(G.ref_rows('ff_d4_s2000.jsonl'))]
+    ops, off, _ = P.compile_strings(pd_, strs)
+    g = _ctx_with_env(pd_.problem_id, {})
+    d = _ctx_with_env(pd_.problem_id, {'PDEVAL_GRAPH': '0'})
+    small = gather_programs(ops, off, np.arange(7))
+    big_idx = np.arange(20000) % len(strs)
+    big = gather_programs(ops, off, big_idx)
+    keys = ('status', 'verdict', 'q_ref', 'res_ref', 'q_grid', 'n_bad', 'n_nonfinite', 'fingerprint')
+    try:
+        want = d.validate(*small)
+        for step in ('capture', 'direct', 'replay', 'device', 'replay'):
+            if step == 'direct':
+                big_out = g.validate(*big)
+                assert np.array_equal(np.asarray(big_out['status']), np.asarray(d.validate(*big)['status']))
+                continue
+            if step == 'device':
+                _device_outputs(g, big[0], big[1], g.n_ref)   # asserts the error word itself
+                continue
+            got = g.validate(*small)
+            assert g.device_error() == 0, step
+            for k in keys:
+                x = np.asarray(got[k])
+                assert np.array_equal(x, np.asarray(want[k]), equal_nan=x.dtype.kind == 'f'), (step, k)
     finally:
         g.close()
         d.close()

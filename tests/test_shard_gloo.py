@@ -159,3 +159,72 @@ def test_two_rank_gather_of_final_verdicts(case, tmp_path):
         assert int((fin['status'] != r['status']).sum()) >= 3
     if case == 'ff_edge_d2':
         assert int((raw & ~single).sum()) >= 1                     # the symbolic zero gradient
+
+
+_OMEGA_STRS = ['rho**2', 'rho**2*exp(-2*z)', 'z + log(1 - rho**2/9)', 'rho**2/(rho**2 + z**2)**(3/2)']
+
+
+def _omega_rows(keys):
+    """Device-style outputs for _OMEGA_STRS[keys]: every row a grid zero (ACCEPT), distinct
+    fingerprint values (no zero-gradient re-check), as the strict / replay modes receive them."""
+    from pdeval.opcodes import CLS_ACCEPT
+    n = len(keys)
+    strs = [_OMEGA_STRS[k] for k in keys]
+    ops, off, _ = P.compile_strings(P.force_free(), strs)
+    r = {'status': np.full(n, CLS_ACCEPT, dtype=np.uint8), 'verdict': np.ones(n, dtype=bool),
+         'q_ref': np.zeros(n), 'res_ref': np.zeros((n, 1)), 'q_grid': np.zeros(n),
+         'n_bad': np.zeros(n, dtype=np.int32), 'n_nonfinite': np.zeros(n, dtype=np.int32),
+         'fingerprint': (np.arange(4 * n, dtype=np.float64).reshape(n, 4) + 1.0)}
+    return strs, ops, off, r
+
+
+def _omega_rank_main(rank, world, port, keys, out_dir):
+    import torch
+    import torch.distributed as dist
+    from pdeval import _lib
+    from pdeval.shard import final_verdicts, _gather
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        strs, ops, off, r = _omega_rows(keys)
+        ranges = shard_ranges(len(strs), world)
+        s, e = ranges[rank]
+        sub = {k: v[s:e].copy() for k, v in r.items()}
+        o, f = _gather(ops, off, np.arange(s, e))
+        fin = final_verdicts(P.force_free(), None, _lib.default_params(0), 4096, strs[s:e], sub, o, f,
+                             keys=np.asarray(keys[s:e]), symbolic='replay', omega='1/3')
+        allv = gather_verdicts(torch.from_numpy(pack_bits(fin)), ranges)
+        np.save(os.path.join(out_dir, f'omega_rank{rank}.npy'), allv)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_final_verdicts_forward_omega(tmp_path):
+    """the multi-rank final verdicts replay the reference's symbolic stage at the
+    plugin's Omega (BatchValidator.omega), not at 0.  Rotating solutions at Omega = 1/3
+    (tests/golden/ref/ff_omega13_known.jsonl: the reference accepts them symbolically) stay
+    accepted through final_verdicts(..., omega='1/3') on the keyed (duplicate-program) path,
+    equal the single-process apply_host_steps, and the 2-rank gloo gather gives the same bits.
+    Bent and Dipolar -- solutions at Omega = 0, rejected by the reference at 1/3 -- are
+    rejected by the replay at 1/3 and accepted at 0 (the bug would have accepted them)."""
+    import torch.multiprocessing as mp
+    from pdeval import _lib
+    from pdeval.batch import apply_host_steps
+    from pdeval.shard import final_verdicts
+    ref = {r['expr']: r['ok'] for r in G.ref_rows('ff_omega13_known.jsonl')}
+    assert [ref[s] for s in _OMEGA_STRS] == [True, False, True, False]
+    keys = [0, 1, 2, 3, 1, 0, 2, 1]
+    prm = _lib.default_params(0)
+    strs, ops, off, r = _omega_rows(keys)
+    got = final_verdicts(P.force_free(), None, prm, 4096, strs, {k: v.copy() for k, v in r.items()}, ops, off,
+                         keys=np.asarray(keys), symbolic='replay', omega='1/3')
+    single = {k: v.copy() for k, v in r.items()}
+    apply_host_steps(P.force_free(), None, prm, 4096, strs, single, ops, off, 'replay', omega='1/3')
+    assert np.array_equal(got, single['verdict'])
+    assert got.tolist() == [ref[_OMEGA_STRS[k]] for k in keys]
+    at0 = final_verdicts(P.force_free(), None, prm, 4096, strs, {k: v.copy() for k, v in r.items()}, ops, off,
+                         keys=np.asarray(keys), symbolic='replay')
+    assert at0.all()
+    mp.spawn(_omega_rank_main, args=(2, _free_port(), keys, str(tmp_path)), nprocs=2, join=True)
+    for k in range(2):
+        assert np.array_equal(np.load(tmp_path / f'omega_rank{k}.npy'), got), k
