@@ -230,6 +230,15 @@ int pdeval_validate_device(pdeval_ctx* ctx, const int32_t* d_ops, int64_t n_word
                            const int64_t* d_offsets, int64_t n, const pdeval_params* params,
                            const pdeval_outputs* d_out, void* stream, int zero_bits);
 
+/* The device error word of the most recent pdeval_validate_device call on this context: call
+ * it after the caller has synchronized that call's stream.  *word = 0 and PDEVAL_OK when the
+ * call was clean; otherwise *word holds the kernel families whose check failed -- a work-list
+ * entry outside [0, n) (skipped), or 0x100: a wave found no free hoist-buffer slot -- the
+ * call's outputs are not to be trusted, and the return is PDEVAL_ERR_HIP with
+ * pdeval_last_error describing the call's state.  (pdeval_validate_batch checks the same
+ * word itself before it returns.)                                                         */
+int pdeval_device_error(pdeval_ctx* ctx, uint32_t* word);
+
 /* Per-pass device timing (bench / profiling).  With timing enabled, pdeval_validate_device
  * records a HIP event before each of its PDEVAL_N_PASSES launches and one after the last, on
  * the launch stream (passes a problem does not run take 0 ms).  pdeval_pass_times waits for

@@ -113,15 +113,19 @@ struct pdeval_ctx {
     uint8_t* d_pstate = nullptr;    // point-stage state, capacity cap
     int32_t* d_dec = nullptr;       // decoded programs of the lean grid passes, dec_cap words
     int64_t dec_cap = 0;
-    // the hoisted x-only prefixes of the lean passes (pdeval_grid.h PD_HOIST): cap x (K + 1) x 64
-    // doubles (env PDEVAL_HOIST=0: none, A/B)
+    // the hoisted prefixes / segments of the lean passes (pdeval_grid.h PD_HOIST): 8 x
+    // kHoistPool slots of hoist_stride doubles and their owner words, whatever the batch size
+    // (env PDEVAL_HOIST=0: none, A/B)
     bool hoist = true;
     bool hoist_sub = true;              // env PDEVAL_HOIST_SUB=0: no hoisted segments (A/B)
     double* d_hoist = nullptr;
+    uint32_t* d_hoist_own = nullptr;
+    bool hoist_slots = true;            // env PDEVAL_HOIST_SLOTS=0: one slot per candidate (A/B)
     int32_t* d_hseg = nullptr;          // the decoder's hoisted segments, cap x 4 words
     // the lean passes' failing lanes per candidate and grid chunk, cap x chunks words, which
     // tier 2 re-checks instead of the whole grid (env PDEVAL_TIER2_MASK=0: none, A/B)
     bool tier2_mask = true;
+    uint64_t* d_fsum = nullptr;         // ... and per candidate the chunks whose word was stored
     int deep_parts = PD_DEEP_PARTS;     // the stack-8 lists' waves per candidate (env PDEVAL_DEEP_PARTS)
     uint64_t* d_fmask = nullptr;
     uint8_t* d_status = nullptr;    // classes when the caller asks for no status output
@@ -444,6 +448,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_LIST_PARTS")) c->list_parts = std::min(16, std::max(1, atoi(v)));
     if (const char* v = getenv("PDEVAL_HOIST")) c->hoist = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_HOIST_SUB")) c->hoist_sub = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_HOIST_SLOTS")) c->hoist_slots = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_TIER2_MASK")) c->tier2_mask = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_DEEP_PARTS")) c->deep_parts = atoi(v) > 1 ? PD_DEEP_PARTS : 1;
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
@@ -482,8 +487,10 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
     if (c->d_ddps) (void)hipFree(c->d_ddps);
     if (c->d_dec) (void)hipFree(c->d_dec);
     if (c->d_hoist) (void)hipFree(c->d_hoist);
+    if (c->d_hoist_own) (void)hipFree(c->d_hoist_own);
     if (c->d_hseg) (void)hipFree(c->d_hseg);
     if (c->d_fmask) (void)hipFree(c->d_fmask);
+    if (c->d_fsum) (void)hipFree(c->d_fsum);
     if (c->d_status) (void)hipFree(c->d_status);
     if (c->d_noise) (void)hipFree(c->d_noise);
     if (c->d_t2acc) (void)hipFree(c->d_t2acc);
@@ -778,21 +785,33 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (c->d_ddps) (void)hipFree(c->d_ddps);
     c->d_ddps = nullptr;
     HIPCHK(c, hipMalloc(&c->d_ddps, cap));
-    if (c->d_hoist) (void)hipFree(c->d_hoist);
-    c->d_hoist = nullptr;
     if (c->d_hseg) (void)hipFree(c->d_hseg);
     c->d_hseg = nullptr;
     if (c->hoist) {
-        // per candidate: the prefix's pure coefficients (K + 1 rows of 64) and the segment's
-        // whole jet (nc(K) rows of 64, Kerr only) -- pd::hoist_stride
+        // per slot (8 pools of kHoistPool, one per XCD; pdeval_grid.h hoist_acquire): the
+        // prefix's pure coefficients (K + 1 rows of 64) and the segment's whole jet (nc(K) rows
+        // of 64, Kerr only) -- pd::hoist_stride; allocated once, it does not grow with the batch
         const int K = c->problem == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
-        HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)cap * pd::hoist_stride(K) * sizeof(double)));
+        if (c->hoist_slots && !c->d_hoist) {
+            HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)8 * pd::kHoistPool * pd::hoist_stride(K) * sizeof(double)));
+            HIPCHK(c, hipMalloc(&c->d_hoist_own, (size_t)8 * pd::kHoistPool * sizeof(uint32_t)));
+            HIPCHK(c, hipMemset(c->d_hoist_own, 0, (size_t)8 * pd::kHoistPool * sizeof(uint32_t)));   // all free
+        } else if (!c->hoist_slots) {   // (A/B: the round-5 layout, one slot per candidate)
+            if (c->d_hoist) (void)hipFree(c->d_hoist);
+            c->d_hoist = nullptr;
+            HIPCHK(c, hipMalloc(&c->d_hoist, (size_t)std::max<int64_t>(cap, 8 * pd::kHoistPool) * pd::hoist_stride(K) * sizeof(double)));
+        }
+        // the decoder's per-candidate segment records
         HIPCHK(c, hipMalloc(&c->d_hseg, (size_t)cap * 4 * sizeof(int32_t)));
     }
     if (c->d_fmask) (void)hipFree(c->d_fmask);
     c->d_fmask = nullptr;
-    if (c->tier2_mask)
+    if (c->d_fsum) (void)hipFree(c->d_fsum);
+    c->d_fsum = nullptr;
+    if (c->tier2_mask) {
         HIPCHK(c, hipMalloc(&c->d_fmask, (size_t)cap * c->nx * (c->ny / 64) * sizeof(uint64_t)));
+        HIPCHK(c, hipMalloc(&c->d_fsum, (size_t)cap * sizeof(uint64_t)));
+    }
     if (c->d_status) (void)hipFree(c->d_status);
     c->d_status = nullptr;
     HIPCHK(c, hipMalloc(&c->d_status, cap));
@@ -952,8 +971,11 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.t2acc = c->d_t2acc;
     a.dec = c->d_dec;
     a.hoist = c->nx <= 64 ? c->d_hoist : nullptr;   // (one grid row per lane)
+    a.hoist_own = c->hoist_slots ? c->d_hoist_own : nullptr;
+    a.hoist_pool = pd::kHoistPool;
     a.hseg = a.hoist && c->hoist_sub ? c->d_hseg : nullptr;
     a.fmask = c->d_fmask;
+    a.fsum = c->d_fsum;
     // ---- the point stage (pdeval_point.h), decided for every candidate before the grid
     // pass 0: real programs of stack <= 2, one candidate per lane; deeper ones -> L_PDEEP,
     // complex-valued ones -> L_CPLX.  Lanes take the candidates sorted by opcode sequence
@@ -1222,7 +1244,8 @@ static int check_errw(pdeval_ctx* c, uint32_t w, const char* path = "direct", in
     for (int k = 0; k < PD_N_LISTS; ++k) cnt += (k ? "," : "") + std::to_string(h[k]);
     char buf[256];
     std::snprintf(buf, sizeof(buf),
-                  "device work-list check failed (kernel families 0x%x): a list entry outside the batch [%s n=%lld "
+                  "device work-list check failed (kernel families 0x%x; 0x100: no free hoist slot): a list entry "
+                  "outside the batch [%s n=%lld "
                   "captured=%d cap=%lld epoch=%llu graphs=%zu counts=",
                   (unsigned)w, path, (long long)n, captured, (long long)c->cap, (unsigned long long)c->buf_epoch,
                   c->graphs.size());

@@ -959,6 +959,67 @@ __device__ __forceinline__ void hoist_parts(const int32_t* dec, int& hoist, bool
     __threadfence_block();   // the rows read other lanes' values
 }
 
+// ---- hoist-buffer slots.  The hoisted parts of a candidate are needed only while its wave runs,
+// so the buffer holds slots, not candidates: 8 pools (one per XCD, so that a slot's successive
+// owners share one L2 -- the XCD L2s are not coherent with each other) of a.hoist_pool slots, more
+// than the waves an XCD holds at once.  A wave takes the slot of its candidate within its pool
+// (linear probing past slots other waves still hold) with a compare-and-swap on the slot's owner
+// word and frees it when its rows are done; its new owner writes every value it reads before
+// reading it.  The buffer stays 30 MiB (force-free) / 54 MiB (Kerr) at any batch size and mostly
+// in L2 / MALL: force-free pass 1 wrote the 2.5 KiB of every hoisted candidate to HBM before
+// (round 5: n x 2.5 KiB, 5.4 GB at 2^21).  A split launch (a small batch's parts: several waves
+// per candidate) indexes by candidate instead (n < 1024 <= the slot count).
+#ifndef PD_HOIST_SLOTS
+#define PD_HOIST_SLOTS 1
+#endif
+// the failing-lane words of tier 1 stored sparsely (a.fsum; see grid_body)
+#ifndef PD_FMASK_SPARSE
+#define PD_FMASK_SPARSE 1
+#endif
+__device__ __forceinline__ uint32_t xcc_id() {
+#ifndef PD_HOST_SIM
+    // HW_REG_XCC_ID (hwreg 20), bits 3:0
+    return (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
+#else
+    return 0u;
+#endif
+}
+// the slot of wave-uniform `cand` (lane 0 takes it; every lane gets it), or -1 when there is no
+// hoist buffer.  A wave that cannot take a slot after every probe of many sweeps (it cannot
+// happen while a pool has more slots than an XCD holds waves) sets ERRW_HOIST and uses its
+// home slot: the call then reports an error rather than hanging
+__device__ __forceinline__ int64_t hoist_acquire(const KernelArgs& a, int64_t cand, int lane, bool split) {
+    if (!PD_HOIST_SLOTS || !a.hoist_own) return cand;   // one slot per candidate (A/B layout)
+    if (split || a.hoist_pool <= 0) {
+        if (cand < (int64_t)8 * a.hoist_pool) return cand;
+        if (lane == 0 && a.errw) atomicOr(a.errw, (uint32_t)ERRW_HOIST);
+        return 0;
+    }
+    const int64_t P = a.hoist_pool, base = (int64_t)xcc_id() * P, home = cand % P;
+    int got = -1;
+    if (lane == 0) {
+        for (int k = 0; k < 64 * kHoistPool && got < 0; ++k) {
+            const int64_t t = base + (home + k) % P;
+            if (atomicCAS(a.hoist_own + t, 0u, 1u) == 0u) got = (int)t;
+            else if (k >= 16) __builtin_amdgcn_s_sleep(1);
+        }
+        if (got < 0) {
+            if (a.errw) atomicOr(a.errw, (uint32_t)ERRW_HOIST);
+            got = (int)(base + home);
+        }
+    }
+    return (int64_t)__builtin_amdgcn_readfirstlane(got);
+}
+// every lane's accesses to the slot are complete (vmcnt(0) waits for the wave's loads and
+// stores), then the owner word is cleared
+__device__ __forceinline__ void hoist_release(const KernelArgs& a, int64_t slot, int lane, bool split) {
+    if (!PD_HOIST_SLOTS || split || !a.hoist_own || a.hoist_pool <= 0 || slot < 0) return;
+#ifndef PD_HOST_SIM
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    if (lane == 0) __hip_atomic_store(a.hoist_own + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The grid stage of one candidate (wave-uniform cand), lean interpreter with MAXD slots, jets
 // over T: double, or cplx for the force-free candidates not real at p* (the complex pass, whose
 // point stage point_list_kernel<.., cplx> decided).
@@ -1045,12 +1106,16 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     // other than the value, so a zero's sign changes no result; where a lane carries a
     // non-finite coefficient (0 * inf = NaN in the others) the candidate is not hoisted.
     // (a.nx <= 64, checked by the host, which passes a.hoist = NULL otherwise)
+    int64_t hslot = -1;   // the candidate's hoist-buffer slot while this wave holds it
     if constexpr (!CX && PD_HOIST) {
-        if (hoist || h_at)
+        if (hoist || h_at) {
+            hslot = hoist_acquire(a, cand, lane, parts > 1);
             hoist_parts<K, MAXD, hoist_sub<PROB>()>(a.dec + beg, hoist, PROB != PDEVAL_PROBLEM_FORCE_FREE && hy, h_at, h_to, h_w0, h_y,
-                                 a.gx, a.nx, a.ny, a.ptab, a.hoist + (size_t)cand * hoist_stride(K),
-                                 a.hoist + (size_t)cand * hoist_stride(K) + (K + 1) * 64, lane, stk, y0, inv_y0);
+                                 a.gx, a.nx, a.ny, a.ptab, a.hoist + (size_t)hslot * hoist_stride(K),
+                                 a.hoist + (size_t)hslot * hoist_stride(K) + (K + 1) * 64, lane, stk, y0, inv_y0);
+        }
     }
+    const double* hbuf = a.hoist + (size_t)(hslot < 0 ? 0 : hslot) * hoist_stride(K);
     GridMax<PROB != PDEVAL_PROBLEM_FORCE_FREE> gm;   // (PD_DIVFREE) the lane's running maximum of q
     double qmax = 0.0;
     int nbad = 0, nfin = 0;
@@ -1064,6 +1129,11 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
     }
     if (a.nx > 64) fp_rows = ~0ull;
     // this part's rows: whole groups of W
+    // PD_FMASK_SPARSE: lane 0 stores only the non-zero failing-lane words and, at the end, the
+    // bitmap of the chunks it stored (a.fsum); a split launch (parts > 1), or a grid of more
+    // than 64 chunks, stores every word and an all-ones bitmap
+    const bool fsparse = PD_FMASK_SPARSE && a.fsum && parts == 1 && a.nx * per_row <= 64;
+    uint64_t fsum = 0ull;
     const int groups = (a.nx + W - 1) / W;
     const int row0 = W * (int)((int64_t)groups * part / parts), row1 = min(a.nx, W * (int)((int64_t)groups * (part + 1) / parts));
     for (int row = row0; row < row1; row += W) {
@@ -1109,7 +1179,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
             if constexpr (!kv_late) load_kv();
             J u[W];
             if (!CX && PD_HOIST && hoist) {
-                const double* hb = a.hoist + (size_t)cand * hoist_stride(K);
+                const double* hb = hbuf;
 #pragma unroll
                 for (int q = 0; q < W; ++q) {
 #pragma unroll
@@ -1124,7 +1194,7 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 }
             }
             L::run(a.dec + beg, x, y, inv_x, inv_y, u, stk, lane, pt, hoist ? hoist : 1, 0,
-                   h_at ? a.hoist + (size_t)cand * hoist_stride(K) + (K + 1) * 64 : nullptr, row, a.nx - 1, h_y);
+                   h_at ? hbuf + (K + 1) * 64 : nullptr, row, a.nx - 1, h_y);
             if constexpr (kv_late) load_kv();
 #pragma unroll
             for (int q = 0; q < W; ++q) {
@@ -1143,6 +1213,30 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 if constexpr (!PD_DIVFREE)
                     qv = PD_FAST_SCALED ? scaled_fast(r.res_abs, r.scale)
                                         : PD_SCALED_SEL ? scaled_sel(r.res_abs, r.scale) : scaled(r.res_abs, r.scale);
+                if constexpr (PD_DIVFREE) {
+                    gm.add(r.finite, r.res_abs, r.scale);
+                    grad_nz = grad_nz | (r.finite & !r.grad_zero);
+                    nfin += count_lanes(r.finite);
+                    const uint64_t fm = lane_mask(r.finite & grid_fails(r.res_abs, r.scale, a.prm.tau_grid));
+                    nbad += (int)__popcll(fm);
+                    // the chunk's failing lanes, for tier 2 (a candidate the point stage rejected
+                    // is final and never escalates)
+                    if (a.fmask && (ps & 3) != P0_REJECT && lane == 0) {
+                        const int ch = (row + q) * per_row + sl;
+                        if (!fsparse || fm) a.fmask[cand * (int64_t)(a.nx * per_row) + ch] = fm;
+                        if (fm) fsum |= 1ull << (ch & 63);
+                    }
+                } else {
+                    if (r.finite) {
+                        qmax = fmax(qmax, qv);
+                        if (!r.grad_zero) grad_nz = true;
+                    }
+                    nfin += (int)__popcll(__ballot(r.finite));
+                    nbad += (int)__popcll(__ballot(r.finite && qv > a.prm.tau_grid));
+                }
+                // the fingerprint points of this row, after the counts: its lane-divergent stores
+                // between the point's flags and their ballots made the compiler keep each flag in
+                // a VGPR across them (a select and a compare more per ballot, every point)
                 if (a.out.fingerprint && (row + q >= 64 || ((fp_rows >> (row + q)) & 1ull))) {
 #pragma unroll
                     for (int f = 0; f < PDEVAL_FP_N; ++f) {
@@ -1154,27 +1248,13 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                         }
                     }
                 }
-                if constexpr (PD_DIVFREE) {
-                    gm.add(r.finite, r.res_abs, r.scale);
-                    grad_nz = grad_nz | (r.finite & !r.grad_zero);
-                    nfin += count_lanes(r.finite);
-                    const uint64_t fm = lane_mask(r.finite & grid_fails(r.res_abs, r.scale, a.prm.tau_grid));
-                    nbad += (int)__popcll(fm);
-                    // the chunk's failing lanes, for tier 2 (a candidate the point stage rejected
-                    // is final and never escalates)
-                    if (a.fmask && (ps & 3) != P0_REJECT && lane == 0)
-                        a.fmask[cand * (int64_t)(a.nx * per_row) + (row + q) * per_row + sl] = fm;
-                } else {
-                    if (r.finite) {
-                        qmax = fmax(qmax, qv);
-                        if (!r.grad_zero) grad_nz = true;
-                    }
-                    nfin += (int)__popcll(__ballot(r.finite));
-                    nbad += (int)__popcll(__ballot(r.finite && qv > a.prm.tau_grid));
-                }
             }
         }
     }
+    if constexpr (!CX && PD_HOIST) {
+        if (hslot >= 0) hoist_release(a, hslot, lane, parts > 1);
+    }
+    if (PD_DIVFREE && a.fmask && a.fsum && (ps & 3) != P0_REJECT && lane == 0) a.fsum[cand] = fsparse ? fsum : ~0ull;
     if constexpr (PD_DIVFREE) qmax = gm.q();
     qmax = wave_max(qmax);
     bool grad_any = __any(grad_nz);

@@ -81,12 +81,18 @@ struct KernelArgs {
     int32_t* dec;               // n_words: the programs pre-decoded for the lean grid passes
     uint64_t* fmask;            // lean passes: per candidate and 64-point grid chunk, the lanes
                                 // that failed the tier-1 test (what tier 2 re-checks); NULL = none
+    uint64_t* fsum;             // ... per candidate, the chunks whose fmask word was written (bit
+                                // per chunk, <= 64 chunks; ~0 = every word): the lean passes store
+                                // only the non-zero words
     int32_t* hseg;              // decoder: per candidate {original word, start, end, y?} of its
                                 // hoisted segment (start 0: none; pdeval_grid.h PD_HOIST_SUB)
-    double* hoist;              // lean passes: per candidate (hoist_stride doubles), the pure
-                                // coefficients of its hoisted prefix at every grid row or lane
-                                // and, Kerr, its hoisted segment's jets (pdeval_grid.h PD_HOIST);
-                                // NULL = nothing hoisted
+    double* hoist;              // lean passes: per slot (hoist_stride doubles), the pure
+                                // coefficients of a candidate's hoisted prefix at every grid row
+                                // or lane and, Kerr, its hoisted segment's jets (pdeval_grid.h
+                                // PD_HOIST); NULL = nothing hoisted
+    uint32_t* hoist_own;        // one owner word per slot (0 = free): a running wave holds the
+                                // slot of its candidate (pdeval_grid.h hoist_acquire)
+    int hoist_pool;             // slots per XCD (8 pools); a split launch indexes by candidate
     // the problem's constants per stage (PDEVAL_IMM_PRM; Kerr M, a): point stage (fp64 and
     // double-double) and the constant test / grid stage
     PrmTab<double> prm_pt, prm_grid;
@@ -131,7 +137,7 @@ struct WorkQueue {
 // error word (bit `code`) and the caller skips it, instead of indexing the batch with it.
 enum : uint32_t {
     ERRW_PERM = 1u, ERRW_GRID_LIST = 2u, ERRW_GENERIC = 4u, ERRW_POINT_LIST = 8u, ERRW_DD = 16u,
-    ERRW_DD_APPLY = 32u, ERRW_TIER2 = 64u, ERRW_CPLX = 128u
+    ERRW_DD_APPLY = 32u, ERRW_TIER2 = 64u, ERRW_CPLX = 128u, ERRW_HOIST = 256u
 };
 #ifndef PD_CHECK_LISTS
 #define PD_CHECK_LISTS 1
@@ -154,6 +160,10 @@ struct T2Acc {
 // coefficients and, Kerr (K = 2) only, the segment's nc(K) coefficients, 64 rows (or lanes) each
 // (force-free hoists no segments: 2.5 KiB per candidate instead of 10)
 PD_HD constexpr size_t hoist_stride(int K) { return (size_t)(K + 1 + (K == 4 ? 0 : (K + 1) * (K + 2) / 2)) * 64; }
+// slots of the hoist buffer per XCD: more than the waves one XCD holds at once (32 CUs x 4
+// SIMDs x <= 6 waves/SIMD in pass 1 = 768), so a wave finds a free slot within a few probes;
+// 8 x 1536 slots = 30 MiB force-free, 54 MiB Kerr, whatever the batch size
+constexpr int kHoistPool = 1536;
 
 // Escalation flags (bits 48.. of a tier-2 list entry; the candidate index is the low 48 bits).
 enum : uint32_t {
@@ -643,6 +653,11 @@ struct PointResult {
 #ifndef PD_BSYM
 #define PD_BSYM 1
 #endif
+// the force-free finiteness guards as one maximum of the coefficient magnitudes (ff_epilogue_p)
+#ifndef PD_FF_GUARD_MAX
+#define PD_FF_GUARD_MAX 1
+#endif
+__device__ __forceinline__ double max_abs(double a, double b);
 #ifndef PD_AFMA
 #define PD_AFMA 1
 #endif
@@ -851,8 +866,20 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_p(const T*
     r.scale = S;
     r.grad_zero = is_zero(u[ji(1, 0)]) && is_zero(u[ji(0, 1)]);
     bool fin = finite_(det) & isfinite(S);
+    if constexpr (std::is_same<T, double>::value && PD_FF_GUARD_MAX) {
+        // the 15 coefficient guards as one maximum (PD_FF_GUARD_MAX): max |c| < 2^160 over the
+        // 14 derivative coefficients, and u itself tested on its own.  The same result: a NaN
+        // that v_max drops is in S already -- every derivative coefficient is read by the
+        // magnitude evaluation (A reads c10..c04 but c01, lie1 reads c01), where it makes S
+        // NaN -- and an infinite coefficient wins the maximum.
+        const double* c = reinterpret_cast<const double*>(u);
+        double m = max_abs(max_abs(max_abs(c[1], c[2]), max_abs(c[3], c[4])), max_abs(max_abs(c[5], c[6]), max_abs(c[7], c[8])));
+        m = max_abs(m, max_abs(max_abs(max_abs(c[9], c[10]), max_abs(c[11], c[12])), max_abs(c[13], c[14])));
+        fin = fin & (m < kHugeJet) & jet_coef_ok(u[0]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 15; ++i) fin = fin & jet_coef_ok(u[i]);
+        for (int i = 0; i < 15; ++i) fin = fin & jet_coef_ok(u[i]);
+    }
     r.finite = fin;
     return r;
 }

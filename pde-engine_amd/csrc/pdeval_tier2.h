@@ -528,9 +528,17 @@ __global__ __launch_bounds__(64, PD_T2_WAVES_PER_SIMD) void tier2_kernel(KernelA
             const int ch1 = (int)((int64_t)nchunks * (part + 1) / PARTS);
             // (packing the failing points 64 to a batch, x per lane, measured slower: force-free
             // tier 2 7.9 vs 6.5 ms, Kerr 2.1 vs 1.3 ms, profiles/r05_n_ab_*.log)
+            // the chunks pass 1 stored a word for (a.fsum: the others had no failing lane)
+            uint64_t stored = ~0ull;
+            if (masked && a.fsum) {
+                const uint64_t v = a.fsum[cand];
+                stored = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+            }
             for (int ch = ch0; ch < ch1; ++ch) {
                 uint64_t m = ~0ull;
                 if (masked) {
+                    if (nchunks <= 64 && !((stored >> ch) & 1ull)) continue;
                     const uint64_t v = a.fmask[cand * (int64_t)nchunks + ch];
                     m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);

@@ -26,6 +26,7 @@ thread past its bound.
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
 import multiprocessing as mp
 import os
 import queue as _queue
@@ -73,6 +74,7 @@ def _call_bounded(fn, x, item_timeout, default):
         return _call_on_thread(fn, x, item_timeout, default)
     old = signal.signal(signal.SIGALRM, _alarm)
     prev = signal.setitimer(signal.ITIMER_REAL, float(item_timeout))
+    t0 = time.monotonic()
     try:
         try:
             r = fn(x)
@@ -86,10 +88,20 @@ def _call_bounded(fn, x, item_timeout, default):
     finally:
         signal.signal(signal.SIGALRM, old)
         if prev[0] > 0:
-            signal.setitimer(signal.ITIMER_REAL, *prev)
+            # an outer timer keeps its deadline: re-armed with what is left of it
+            signal.setitimer(signal.ITIMER_REAL, max(prev[0] - (time.monotonic() - t0), 1e-3), prev[1])
+
+
+_ABANDONED: List[threading.Thread] = []
+MAX_ABANDONED = 4     # bounded calls left running past their bound, at most (they hold the GIL)
 
 
 def _call_on_thread(fn, x, item_timeout, default):
+    # once MAX_ABANDONED timed-out calls are still running, further items take their default
+    # without starting another thread that would compete for the GIL with the pipeline threads
+    _ABANDONED[:] = [t for t in _ABANDONED if t.is_alive()]
+    if len(_ABANDONED) >= MAX_ABANDONED:
+        return default
     box = []
 
     def body():
@@ -102,6 +114,7 @@ def _call_on_thread(fn, x, item_timeout, default):
     t.start()
     t.join(float(item_timeout))
     if not box:
+        _ABANDONED.append(t)
         return default
     ok, v = box[0]
     if not ok:
@@ -151,6 +164,7 @@ class _FixedPool:
         self.job = 0
         self.lock = threading.Lock()
         self.inbox = {}                      # job -> queue.Queue of (k, ok, out)
+        self.futures = {}                    # job -> (Future, deadline, default): submit()
         self._stop = False
         self.collector = threading.Thread(target=self._collect, daemon=True)
         self.collector.start()
@@ -163,13 +177,50 @@ class _FixedPool:
                 if not self._stop and not all(p.is_alive() for p in self.procs):
                     self._break()
                     return
+                self._expire()
                 continue
             except (EOFError, OSError):
                 return
             with self.lock:
                 box = self.inbox.get(j)
+                fut = self.futures.pop(j, None)
             if box is not None:
                 box.put((k, ok, out))
+            elif fut is not None and not fut[0].done():
+                fut[0].set_result(out[0] if ok else fut[2])
+            self._expire()
+
+    def _expire(self):
+        """submit()'s futures past their deadline (a child stuck in a C-level call that SIGALRM
+        cannot interrupt) resolve to their default."""
+        now = time.monotonic()
+        with self.lock:
+            late = [j for j, (_f, dl, _d) in self.futures.items() if dl is not None and now > dl]
+            got = [self.futures.pop(j) for j in late]
+        for f, _dl, d in got:
+            if not f.done():
+                self.overdue += 1
+                f.set_result(d)
+
+    def submit(self, fn, x, item_timeout=None, default=None) -> cf.Future:
+        """fn(x) in a child, as a Future (resolved by the collector thread): the streaming
+        callers' form of map_chunks.  With an ``item_timeout`` the item yields ``default`` at its
+        bound in the child, and the Future resolves to ``default`` at a deadline that counts
+        the items queued before it (spread over the children) plus a margin."""
+        fut: cf.Future = cf.Future()
+        with self.lock:
+            if self.broken:
+                fut.set_result(default)
+                return fut
+            self.job += 1
+            job = self.job
+            dl = None
+            if item_timeout:
+                ahead = len(self.futures) + 1
+                dl = time.monotonic() + float(item_timeout) * (ahead / max(1, self.n) + 1) + DEADLINE_MARGIN_S
+            self.futures[job] = (fut, dl, default)
+        self.tasks.put((job, 0, fn, [x], item_timeout, default))
+        return fut
 
     def map_chunks(self, fn, chunks, item_timeout=None, default=None) -> list:
         """Per chunk: its result list, or None where the pool could not deliver it (a child
@@ -212,6 +263,12 @@ class _FixedPool:
     def _break(self):
         self.broken = True
         self.close(graceful=False)
+        with self.lock:
+            got = list(self.futures.values())
+            self.futures.clear()
+        for f, _dl, d in got:      # (a dead child: the streaming callers keep the default)
+            if not f.done():
+                f.set_result(d)
 
     def close(self, graceful: bool = True):
         if graceful and not self.broken:
@@ -276,6 +333,21 @@ def run(fn, items, min_items: int = 8, item_timeout: Optional[float] = None, def
     for ch, part in zip(chunks, parts):
         out.extend(part if part is not None else [_call_bounded(fn, x, item_timeout, default) for x in ch])
     return out
+
+
+_LOCAL = None      # submit() without the pool: a few helper threads (SymPy holds the GIL anyway)
+
+
+def submit(fn, x, item_timeout: Optional[float] = None, default=None) -> cf.Future:
+    """fn(x) as a Future: in a pool child when the pool runs (``_FixedPool.submit``), else on a
+    small in-process thread pool, bounded by ``item_timeout`` as ``run`` bounds it off the main
+    thread.  For the streaming strict mode (pdeval.worker): items resolve as they finish."""
+    global _LOCAL
+    if active():
+        return _POOL.submit(fn, x, item_timeout, default)
+    if _LOCAL is None:
+        _LOCAL = cf.ThreadPoolExecutor(max_workers=2, thread_name_prefix='pdeval-submit')
+    return _LOCAL.submit(_call_bounded, fn, x, item_timeout, default)
 
 
 def _compile_chunk(args):

@@ -202,6 +202,20 @@ def suspect(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol) -> bool:
     return False
 
 
+# the string forms through which a candidate's SymPy tree can get a non-integer power or an Abs
+# (the only nodes suspect() looks for): the unary ops whose exponent is fractional, sqrt,
+# an explicit Abs, a parenthesised exponent (p/q), a float
+_SUSPECT_TOKENS = ('sqrt', 'pow_3_2', 'pow_neg_3_2', 'Abs', '**(', '.')
+
+
+def may_be_suspect(s: str) -> bool:
+    """A necessary condition for :func:`suspect` on the candidate string, without SymPy: a
+    string with none of these tokens parses to a tree of integer powers, exp and the four
+    arithmetic operations only, which suspect() never flags (the streaming strict mode,
+    pdeval.worker, keeps the device's verdict for it without a pool round trip)."""
+    return any(t in s for t in _SUSPECT_TOKENS)
+
+
 _PDS: Dict[str, object] = {}
 
 

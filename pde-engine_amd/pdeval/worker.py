@@ -268,9 +268,11 @@ def _symbolic_args(validator) -> dict:
     return fn() if fn is not None else {}
 
 
-def _results(claimed, p, t, locs, tagger):
+def _results(claimed, p, t, locs, tagger, hold=None):
     """Result tuples of one batch from its compile (p) and its verdict table (t): errors
-    first, then the completed rows in claim order (the order process_batch has always used)."""
+    first, then the completed rows in claim order (the order process_batch has always used).
+    ``hold`` (optional, bool[n]): rows left out of the list, returned as {row: tuple} beside it
+    (the streaming strict mode emits them when their replay resolves)."""
     from itertools import repeat
     from .native import COMPILE_PARSE
     cst = p.get('compile_status')
@@ -294,6 +296,14 @@ def _results(claimed, p, t, locs, tagger):
         if tagged:
             is_paper[i], names[i] = True, name
     rows = zip(repeat('completed'), ok.tolist(), reasons, is_paper, names, ids)
+    if hold is not None:
+        held = {}
+        for i, (r, d, h) in enumerate(zip(rows, drop.tolist(), hold.tolist())):
+            if h and not d:
+                held[i] = r
+            elif not d:
+                results.append(r)
+        return results, held
     if drop.any():
         results.extend(r for r, d in zip(rows, drop.tolist()) if not d)
     else:
@@ -301,7 +311,77 @@ def _results(claimed, p, t, locs, tagger):
     return results
 
 
-def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, compilers: int = 4):
+class StrictStream:
+    """The 'strict' symbolic mode of the worker pipeline, streamed: a batch's
+    rows are emitted at device rate except its grid zeros of a possibly suspect shape
+    (pdeval.symbolic.may_be_suspect, a string test), which go to the SymPy pool one by one
+    (pdeval.symbolic.strict_str: the shape test, then the reference's symbolic stage replayed
+    under the per-candidate bound) and are emitted when their task resolves.  Each row's final
+    tuple is the one the batch-synchronous strict mode gives (pdeval.batch._strict_stage): a
+    replay's verdict and text, 'keep' / a timeout / a SymPy failure the device's; a row the
+    replay turns valid gets its known-solution tag from its fingerprint then.  ``stats``:
+    grid zeros, rows sent to the pool, suspects, replays, timeouts."""
+
+    def __init__(self, bv, tagger, timeout: float):
+        import threading
+        from collections import deque
+        self.bv, self.tagger, self.timeout = bv, tagger, timeout
+        self.pending = deque()   # (future, held tuple, string, fingerprint, device ok)
+        self.lock = threading.Lock()   # split() runs on the pipeline's result thread
+        self.stats = {'grid_zero': 0, 'sent': 0, 'suspect': 0, 'replayed': 0, 'timeouts': 0}
+
+    def split(self, claimed, p, t, locs):
+        """Ready tuples of one batch (finished with symbolic='off'); its held rows are queued."""
+        from .opcodes import CLS_ACCEPT, CLS_REJECT_SYMBOLIC
+        from . import symbolic as S
+        st = np.asarray(t['status'])
+        strs = p['strings']
+        gz = np.isin(st, (CLS_ACCEPT, CLS_REJECT_SYMBOLIC))
+        self.stats['grid_zero'] += int(gz.sum())
+        hold = gz & np.fromiter((S.may_be_suspect(x) for x in strs), dtype=bool, count=len(strs))
+        ready, held = _results(claimed, p, t, locs, self.tagger, hold)
+        fp = np.asarray(t['fingerprint']).reshape(len(st), -1)
+        for i, row in held.items():
+            self.stats['sent'] += 1
+            fut = hostpool.submit(S.strict_str, (self.bv.pd.slug, strs[i], self.bv.omega),
+                                  item_timeout=self.timeout, default='timeout')
+            with self.lock:
+                self.pending.append((fut, row, strs[i], fp[i], bool(t['ok'][i])))
+        return ready
+
+    def _final(self, r, row, s, fp, dev_ok):
+        if r == 'keep' or r is None:
+            return row
+        self.stats['suspect'] += 1
+        if r == 'timeout':
+            self.stats['timeouts'] += 1
+            return row
+        self.stats['replayed'] += 1
+        ok, text = r
+        tagged, name = (row[3], row[4]) if (ok and dev_ok) else (False, None)
+        if ok and not dev_ok:
+            tagged, name = self.tagger.tag([s], fps=np.asarray([fp]))[0]
+        return (row[0], bool(ok), text, tagged, name, row[5])
+
+    def drain(self, wait: bool = False):
+        """The held rows resolved so far (all of them with wait=True), as one tuple list."""
+        with self.lock:
+            items = list(self.pending)
+            self.pending.clear()
+        out, keep = [], []
+        for it in items:
+            if wait or it[0].done():
+                out.append(self._final(it[0].result(), *it[1:]))
+            else:
+                keep.append(it)
+        if keep:
+            with self.lock:
+                self.pending.extendleft(reversed(keep))
+        return out
+
+
+def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, compilers: int = 4,
+                    stream_strict: bool = True, stats: Optional[dict] = None):
     """process_batch over an iterable of claimed batches, pipelined in four stages on their own
     threads: the next batches compile on the host (``compilers`` threads, so that one batch's
     native compile -- C++ threads, GIL released -- overlaps another's wait for the SymPy pool),
@@ -312,7 +392,12 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, co
     waits overlap instead of adding up (r04_e profile: finish 0.071 s + results 0.097 s per
     142 k rows on one thread was the pipeline's critical path).  ``depth`` batches are in
     flight at most.  Yields each batch's result tuples, in order, identical to
-    process_batch's.  An empty or None batch (the queue is idle) flushes."""
+    process_batch's.  An empty or None batch (the queue is idle) flushes.
+
+    In the 'strict' symbolic mode (``stream_strict``, the default) the replays do not hold
+    their batch: each batch yields its other rows at once, and the held rows come later in
+    lists of their own as their replays resolve (:class:`StrictStream`) -- the same tuples as
+    process_batch's, in another order; ``stats`` (a dict) receives the mode's counts."""
     if not (hasattr(validator, 'validate_strings') and not kwargs.get('check_regularity', False)
             and not kwargs.get('fast_point_only', False)):
         for claimed in batches:
@@ -323,6 +408,10 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, co
     from concurrent.futures import ThreadPoolExecutor
     bv = validator._validator()
     sym = _symbolic_args(validator)
+    strict = None
+    if stream_strict and sym.get('symbolic') == 'strict' and bv.pd.slug == 'force_free':
+        strict = StrictStream(bv, tagger, sym.get('symbolic_timeout') or bv.symbolic_timeout)
+        sym = {**sym, 'symbolic': 'off'}
 
     # each stage is one thread and takes its batches in submission order, so a stage only ever
     # waits for an earlier stage's future of the same batch
@@ -336,21 +425,35 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, co
 
     def res(claimed, ff):
         p, t = ff.result()
+        if strict is not None:
+            return strict.split(claimed, p, t, locs)
         return _results(claimed, p, t, locs, tagger)
 
     with ThreadPoolExecutor(max_workers=max(1, compilers)) as comp, ThreadPoolExecutor(max_workers=1) as dev, \
             ThreadPoolExecutor(max_workers=1) as fins, ThreadPoolExecutor(max_workers=1) as outs:
         inflight = deque()    # futures of each batch's result tuples
 
+        def resolved(wait=False):
+            if strict is not None:
+                done = strict.drain(wait)
+                if done:
+                    yield done
+
         for claimed in batches:
             if not claimed:
                 while inflight:
                     yield inflight.popleft().result()
+                yield from resolved(wait=True)
                 continue
             pf = comp.submit(bv.prepare_strings, [s for _, s in claimed])
             ff = fins.submit(fin, dev.submit(run, pf))
             inflight.append(outs.submit(res, claimed, ff))
             while len(inflight) > depth:
                 yield inflight.popleft().result()
+            yield from resolved()
         while inflight:
             yield inflight.popleft().result()
+            yield from resolved()
+        yield from resolved(wait=True)
+    if strict is not None and stats is not None:
+        stats.update(strict.stats)

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Per-opcode cost model of the pass-1 kernel on the GPU: batches of one repeated program,
 pass times from the library's events.
-Usage: python scripts/microbench.py [--n N] [--problem force_free|kerr_magnetosphere]"""
+Usage: python scripts/microbench.py [--n N] [--problem force_free|kerr_magnetosphere] [--set calib]
+
+--set calib: one program per opcode the FLOP model prices (scripts/flop_calib.py turns their
+PMC FP64 counts, scripts/gpu_pmc_micro.sh, into the executed-flop table of the model)."""
 import argparse
 import os
 import sys
@@ -18,12 +21,33 @@ KERR_PROGS = ['r', 'x', 'r*x', 'r + x', 'r*x*x', 'r*x + r', '-r + 3', '3*r*x', '
               'exp(-r)*x', 'sqrt(r + x)', '(r + x)**(3/2)', '(r + x)**(-3/2)', 'log(r + x)', 'r**2*x', 'r**3*x',
               'exp(r)*exp(x)', '(r + 2)*(x + 3)', 'M*r + a*x']
 
+# one opcode each on top of a base program of both coordinates (no hoisted prefix: the first
+# opcodes already mix x and y); the base programs themselves come first
+CALIB_FF = ['rho', 'z', 'rho*z', 'rho + z', 'rho - z', '3*rho*z', 'rho*z + 3', 'rho/z', 'z/rho',
+            '(rho + z)*(rho - z)', '(rho + z)/(rho - z + 7)', '(rho + z) - (rho*z + 7)',
+            'exp(rho*z)', 'sqrt(rho*z + 7)', 'log(rho*z + 7)', '(rho*z + 7)**(3/2)', '(rho*z + 7)**(-3/2)',
+            '(rho*z + 7)**(1/4)', '(rho*z)**2', '(rho*z)**3', '(rho*z)**4', '(rho*z)**5', '(rho*z)**7',
+            'rho**2*z', 'rho + z**2', 'rho*z + rho**2', 'rho*z - rho**3', 'rho*z/rho**2', 'rho**2/(rho*z + 7)',
+            'rho**3*z**2', 'Abs(rho*z - 1)', '3/(rho*z + 7)', 'z*rho + z**2']
+CALIB_KERR = ['r', 'x', 'r*x', 'r + x', 'r - x', '3*r*x', 'r*x + 3', 'r/x', 'x/r', '(r + x)*(r - x)',
+              '(r + x)/(r - x + 7)', '(r + x) - (r*x + 7)', 'exp(r*x)', 'sqrt(r*x + 7)', 'log(r*x + 7)',
+              '(r*x + 7)**(3/2)', '(r*x + 7)**(-3/2)', '(r*x + 7)**(1/4)', '(r*x)**2', '(r*x)**3', '(r*x)**4',
+              '(r*x)**5', '(r*x)**7', 'r**2*x', 'r + x**2', 'r*x + r**2', 'r*x - r**3', 'r*x/r**2',
+              'r**2/(r*x + 7)', 'r**3*x**2', 'Abs(r*x - 1)', '3/(r*x + 7)', 'x*r + x**2', 'M*r*x', 'a*r*x']
+
+
+def programs(problem_id: int, which: str):
+    if which == 'calib':
+        return CALIB_FF if problem_id == 0 else CALIB_KERR
+    return PROGS if problem_id == 0 else KERR_PROGS
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--n', type=int, default=1 << 18)
     ap.add_argument('--reps', type=int, default=3)
     ap.add_argument('--problem', default='force_free')
+    ap.add_argument('--set', default='default', choices=['default', 'calib'])
     a = ap.parse_args()
     import torch
     from pdeval import _lib, problem_defs as P
@@ -34,13 +58,21 @@ def main():
     dev = torch.device('cuda:0')
     stream = torch.cuda.Stream(dev)
     n = a.n
-    outs = [torch.zeros(s, dtype=t, device=dev) for s, t in
-            ((((n + 31) // 32) * 4, torch.uint8), (n, torch.uint8), (n, torch.float64), (n, torch.float64),
-             (n * ctx.n_ref, torch.float64), (n, torch.int32), (n, torch.int32), (n * FP_N, torch.float64))]
-    d_out = _lib.Outputs(*[o.data_ptr() for o in outs])
+    # by field name (round 6: the positional list passed an n-double buffer as res_ref, which
+    # holds n x n_ref -- Kerr's 3 reference points wrote past it and faulted the GPU)
+    outs = {'verdict_bits': torch.zeros(((n + 31) // 32) * 4, dtype=torch.uint8, device=dev),
+            'status': torch.zeros(n, dtype=torch.uint8, device=dev),
+            'q_ref': torch.zeros(n, dtype=torch.float64, device=dev),
+            'res_ref': torch.zeros(n * ctx.n_ref, dtype=torch.float64, device=dev),
+            'q_grid': torch.zeros(n, dtype=torch.float64, device=dev),
+            'n_bad': torch.zeros(n, dtype=torch.int32, device=dev),
+            'n_nonfinite': torch.zeros(n, dtype=torch.int32, device=dev),
+            'fingerprint': torch.zeros(n * FP_N, dtype=torch.float64, device=dev)}
+    assert set(outs) == {f for f, _ in _lib.Outputs._fields_}
+    d_out = _lib.Outputs(*[outs[f].data_ptr() for f, _ in _lib.Outputs._fields_])
     prm = _lib.default_params(pd_.problem_id)
     ctx.set_timing(True)
-    for s in (PROGS if pd_.problem_id == 0 else KERR_PROGS):
+    for s in programs(pd_.problem_id, a.set):
         w = np.array(pd_.compile(pd_.parse(s)), dtype=np.int32)
         ops = np.tile(w, n)
         off = np.arange(n + 1, dtype=np.int64) * len(w)

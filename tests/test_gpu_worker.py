@@ -179,3 +179,34 @@ def test_reference_driver_rows_through_worker_and_writer(tmp_path):
         if r['validation_reason'] == 'constant-only (skipped)':
             continue
         assert got[r['id']] == (r['validation_status'], r['is_valid'], r['validation_reason']), r['expression']
+
+
+def test_strict_stream_equals_batch_strict():
+    """the streaming 'strict' mode (worker.StrictStream inside
+    process_batches) emits the same result tuples as the batch-synchronous strict mode
+    (process_batch, whose host steps replay every suspect before the batch returns) -- as a
+    multiset, since held rows come later -- on the depth-5 rows the default mode gets wrong
+    (their replays change verdicts) and a depth-4 sample; the stream's counts add up."""
+    from problems import load_problem
+    from problems.force_free.validator import PreciseFoliationValidator
+    from pdeval.worker import KnownSolutionTagger, process_batch, process_batches
+    prob = load_problem('force_free')
+    locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
+    tagger = KnownSolutionTagger(prob, locs)
+    strs = sorted(G.FF_OFF_MODE_DIVERGENCE) + [r['expr'] for r in G.ref_rows('ff_d4_s500.jsonl')[:150]]
+    strs += list(prob.known_solutions)[:6]
+    claimed = [(i + 1, s) for i, s in enumerate(strs)]
+    v = PreciseFoliationValidator(symbolic='strict')
+    kw = {'check_regularity': False, 'fast_point_only': False}
+    sync = []
+    for k in range(0, len(claimed), 64):
+        sync.extend(process_batch(claimed[k:k + 64], v, kw, locs, tagger))
+    stats = {}
+    got = [t for r in process_batches((claimed[k:k + 64] for k in range(0, len(claimed), 64)), v, kw, locs,
+                                      tagger, stats=stats) for t in r]
+    assert sorted(got, key=lambda t: t[5]) == sorted(sync, key=lambda t: t[5])
+    assert len(got) == len(claimed)
+    assert stats['sent'] >= stats['suspect'] >= stats['replayed'] >= 1
+    assert stats['grid_zero'] >= stats['sent']
+    off = process_batch(claimed, prob.validator, kw, locs, tagger)
+    assert sorted(off, key=lambda t: t[5]) != sorted(got, key=lambda t: t[5])   # the replays changed rows
