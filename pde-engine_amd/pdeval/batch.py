@@ -294,14 +294,23 @@ def _fdiv(a: float, b: float) -> float:
     return a / b
 
 
-def _exp_overflows(words, prm_values, points=_KERR_REF_POINTS) -> bool:
+_FF_REF_POINT = ((0.8, 6 / 7),)   # force-free p* (validator.py:296-297)
+
+
+def _exp_overflows(words, prm_values, points=_KERR_REF_POINTS, magnitude: bool = False) -> bool:
     """Does evaluating the program (values only, fp64, host) at a reference point take exp of
     an argument beyond the fp64 range (|arg| > 708: inf, or 0 / a subnormal that a fractional
     power or a product with an overflowed factor turns into inf or 0 * inf)?  The device's point
     stage then sees a non-finite value where the reference's arbitrary-range evaluation sees a
     finite one.  A non-real
     intermediate (sqrt of a negative value) ends that point's evaluation without an answer;
-    a division by zero gives +-inf or nan, as on the device, and the evaluation goes on."""
+    a division by zero gives +-inf or nan, as on the device, and the evaluation goes on.
+
+    ``magnitude`` (force-free, a point the device found non-finite): True unless a value turns
+    non-finite -- a division by an exact zero, a log of 0: a pole at the point, which the
+    reference's exact evaluation sees too -- or non-real; every value finite and real means the
+    jets' range failed (a coefficient past the device's 2^160 guard: derivatives of e^84 /
+    0.0095, or a fractional power of a tiny value: the higher coefficients of sqrt(e^-403))."""
     for x, y in points:
         st: List[float] = []
         acc = 0.0
@@ -389,10 +398,56 @@ def _exp_overflows(words, prm_values, points=_KERR_REF_POINTS) -> bool:
                     acc = abs(acc)
                 else:
                     break
+                if magnitude and not math.isfinite(acc):
+                    return False              # (a pole: the exact value is not finite either)
                 i += op_len(w)
-        except (ValueError, ZeroDivisionError, OverflowError, IndexError):
+        except OverflowError:
+            if magnitude:
+                return True
             continue
+        except (ValueError, ZeroDivisionError, IndexError):
+            if magnitude:
+                return False                  # (not real there: the complex passes' case)
+            continue
+        if magnitude:
+            # every value finite and real at p*: the device's non-finite point came from the
+            # jets' range -- a coefficient past the 2^160 guard (derivatives of e^84 / 0.0095),
+            # or a fractional power of a tiny value
+            return True
     return False
+
+
+def ff_range_point_check(pd, items, out, ops, off, n_grid: int, full_grid: bool, max_bad: int) -> List[int]:
+    """Force-free point rejects that only the fp64 range caused: the device could not evaluate
+    the determinant at p* (a non-finite value, q_ref not > 0) because an intermediate value of
+    the program there lies beyond the range its jets tolerate (``exp(exp(rho/(1 - z)))``: e^270;
+    ``sqrt(exp_neg(exp(z/(1 - z))))``: sqrt of e^-403, whose higher Taylor coefficients overflow)
+    -- while the reference's exact evaluation (validator.py:349-402) finds the value, 0 for a
+    true solution.  Found by the host's fp64 value interpreter at p* (_exp_overflows with
+    ``magnitude``; a pole at p* is not range trouble and keeps the reject).  The grid stage
+    then decides, as after a passing point stage: no more failing points than ``max_bad`` and
+    at least one finite point -> ACCEPT, else REJECT_GRID (needs full_grid, which evaluates the
+    grid of point rejects).  Measured against the reference's own verdicts on every such row of
+    the depth-4 stream and the depth-5 sample (tests/golden/ref/ff_range_rows.jsonl).  Updates
+    ``out`` in place; returns the changed rows."""
+    if pd.problem_id != PROBLEM_FORCE_FREE or not full_grid:
+        return []
+    st = np.asarray(out['status'])
+    with np.errstate(invalid='ignore'):
+        sel = np.flatnonzero((st == CLS_REJECT_POINT) & ~(np.asarray(out['q_ref']) > 0))
+    rows = []
+    nb = np.asarray(out['n_bad'])
+    nn = np.asarray(out['n_nonfinite'])
+    off = np.asarray(off)
+    for i in sel.tolist():
+        if not _exp_overflows(ops[off[i]:off[i + 1]], (0.0,) * 8, _FF_REF_POINT, magnitude=True):
+            continue
+        ok = int(nb[i]) <= max_bad and n_grid - int(nn[i]) > 0
+        st[i] = CLS_ACCEPT if ok else CLS_REJECT_GRID
+        if 'verdict' in out:
+            out['verdict'][i] = ok
+        rows.append(i)
+    return rows
 
 
 def kerr_exact_point_check(pd, kerr, items, out, ops, off, abs_tol: float = 1e-10,
@@ -655,6 +710,7 @@ def apply_host_steps(pd, kerr, params, n_grid: int, items, r, ops, off, symbolic
     ``r`` is one validate call's outputs (``status``, ``verdict``, ``res_ref``, ``q_ref``,
     ``n_bad``, ``n_nonfinite``, ``fingerprint``); ``n_grid`` the grid's point count.  Needs no
     GPU: the multi-rank path runs it per shard before the gather (pdeval.shard.final_verdicts)."""
+    ff_range_point_check(pd, items, r, ops, off, n_grid, bool(params.full_grid), int(params.max_bad))
     symbolic_zero_gradient(pd, items, r)
     kerr_symbolic_constant(pd, items, r, ops, off)
     kerr_exact_point_check(pd, kerr, items, r, ops, off, params.kerr_abs_tol, n_grid, bool(params.full_grid),

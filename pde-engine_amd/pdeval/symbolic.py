@@ -174,6 +174,53 @@ def ff_point_stage(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol,
     return None if d < 1e-20 else (False, f'Invalid (point check ≈ {d:.2e})')
 
 
+FF_POINT = (sp.Rational(4, 5), sp.Rational(6, 7))   # validator.py:296-297
+
+
+def ff_point_exact(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol, Omega: sp.Basic = sp.Integer(0),
+                   point=FF_POINT) -> Optional[Tuple[bool, str]]:
+    """The reference's zero-gradient test and point stage, statement for statement
+    (validator.py:305-312, :349-402 with fast_point_only off): None when the point stage
+    passes (the symbolic stage comes next), else the reference's (False, reason) -- "Zero
+    gradient (constant expression)", "Invalid (point check != 0)" for a non-zero Number after
+    ``cancel(together(.))`` (nan included), "Invalid (point check ≈ {:.2e})" from
+    ``complex(evalf(50))`` (inf and nan included), "Could not evaluate point check" when that
+    evaluation raises.  Exceptions of the cheap reductions are swallowed, as there.  For the
+    force-free point rejects the device could not evaluate at p* (pdeval.batch.ff_exact_point_check)."""
+    det_M = ff_det(u, rho, z, Omega)
+    if det_M is None:
+        return False, 'Zero gradient (constant expression)'
+    s = det_M.subs({rho: point[0], z: point[1]})
+    try:
+        s = sp.cancel(sp.together(s))
+        if s.is_Number and s != 0:
+            return False, 'Invalid (point check != 0)'
+        s = sp.simplify(s)
+    except Exception:   # noqa: BLE001
+        pass
+    try:
+        d = abs(complex(s.evalf(50)))
+    except Exception:   # noqa: BLE001
+        return False, 'Could not evaluate point check'
+    return None if d < 1e-20 else (False, f'Invalid (point check ≈ {d:.2e})')
+
+
+def ff_point_exact_str(args):
+    """ff_point_exact of a candidate string in a SymPy pool process: ``(slug, expr_str[,
+    Omega])`` -> 'pass', or the reference's (False, reason); None if SymPy fails."""
+    slug, s = args[:2]
+    omega = sp.sympify(args[2]) if len(args) > 2 else sp.Integer(0)
+    from . import problem_defs as P
+    if slug not in _PDS:
+        _PDS[slug] = P.get(slug)
+    pd = _PDS[slug]
+    try:
+        r = ff_point_exact(pd.parse(s), pd.x, pd.y, omega)
+    except Exception:   # noqa: BLE001
+        return None
+    return 'pass' if r is None else r
+
+
 # ------------------------------------------------------------------ 'strict': targeted replay
 def suspect(u: sp.Basic, rho: sp.Symbol, z: sp.Symbol) -> bool:
     """The shapes in which the reference's symbolic stage disagrees with det == 0 on the grid,

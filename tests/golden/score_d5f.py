@@ -7,11 +7,11 @@ Input: the reference's verdicts on ``streams/force_free_d5_faithful.txt.gz`` (th
 
 For every DECIDED row (the reference finished within 20 s) it computes, without a GPU:
   * the default ('off') plugin verdict: the device's class -- the C oracle's, which the GPU
-    parity tests hold equal to the device class for class -- through the host's symbolic
-    zero-gradient step (pdeval.batch.symbolic_zero_gradient), as the product path applies it;
+    parity tests hold equal to the device class for class -- through the host steps the product
+    path applies to force-free rows (pdeval.batch.ff_range_point_check, symbolic_zero_gradient);
   * the 'strict' verdict: the same, and for grid zeros of a suspect shape
-    (pdeval.symbolic.suspect, FROZEN at commit 5708cbc before this sample was drawn; sha256 of
-    pdeval/symbolic.py's rule recorded below) the product's replay of the reference's symbolic
+    (pdeval.symbolic.suspect, FROZEN: its source is the text of commit 5708cbc, from before this
+    sample was drawn; the sha256 of that source is recorded in the summary) the product's replay of the reference's symbolic
     stage (pdeval.symbolic.strict_str, 60 s bound -- past it the device's verdict stands).
 The replays are recorded in ``replay/d5f_replay.jsonl`` (strings and verdicts only), so the CPU
 test re-scores without SymPy; the summary goes to ``ref/d5f_score.json``.
@@ -63,13 +63,14 @@ def score(rs, replays):
     import oracle_lib as O
     from pdeval import problem_defs as P
     from pdeval import symbolic as S
-    from pdeval.batch import symbolic_zero_gradient
+    from pdeval.batch import ff_range_point_check, symbolic_zero_gradient
     from pdeval.opcodes import CLS_ACCEPT, CLS_REJECT_SYMBOLIC
     pd = P.force_free()
     dec = [r for r in rs if r['ok'] is not None]
     strs = [r['expr'] for r in dec]
     ops, off, _ = P.compile_strings(pd, strs)
     ora = O.validate_mt(0, ops, off)
+    ff_range_point_check(pd, strs, ora, ops, off, 4096, True, 0)
     symbolic_zero_gradient(pd, strs, ora)
     zero = np.isin(ora['status'], (CLS_ACCEPT, CLS_REJECT_SYMBOLIC))
     susp = [bool(zero[i]) and S.suspect(pd.parse(s), pd.x, pd.y) for i, s in enumerate(strs)]
@@ -102,7 +103,7 @@ def main():
     from pdeval import symbolic as S
     import oracle_lib as O
     import numpy as np
-    from pdeval.batch import symbolic_zero_gradient
+    from pdeval.batch import ff_range_point_check, symbolic_zero_gradient
     from pdeval.opcodes import CLS_ACCEPT, CLS_REJECT_SYMBOLIC
     rs = rows()
     rp = os.path.join(HERE, 'replay', 'd5f_replay.jsonl')
@@ -116,6 +117,7 @@ def main():
     strs = [r['expr'] for r in dec]
     ops, off, _ = P.compile_strings(pd, strs)
     ora = O.validate_mt(0, ops, off)
+    ff_range_point_check(pd, strs, ora, ops, off, 4096, True, 0)
     symbolic_zero_gradient(pd, strs, ora)
     zero = np.isin(ora['status'], (CLS_ACCEPT, CLS_REJECT_SYMBOLIC))
     need = [s for i, s in enumerate(strs) if zero[i] and s not in replays and S.suspect(pd.parse(s), pd.x, pd.y)]
@@ -129,8 +131,10 @@ def main():
                 if (k + 1) % 20 == 0:
                     print(f'[replay] {k + 1}/{len(need)}', flush=True)
     summ, _ = score(rs, replays)
-    with open(os.path.join(ROOT, 'pde-engine_amd', 'pdeval', 'symbolic.py'), 'rb') as f:
-        summ['symbolic_py_sha256'] = hashlib.sha256(f.read()).hexdigest()
+    # the rule scored, frozen: the source of pdeval.symbolic.suspect, equal to its text at
+    # commit 5708cbc (before the sample was drawn)
+    import inspect
+    summ['suspect_source_sha256'] = hashlib.sha256(inspect.getsource(S.suspect).encode()).hexdigest()
     with open(os.path.join(HERE, 'ref', 'd5f_score.json'), 'w') as f:
         json.dump(summ, f, indent=1)
     print(json.dumps({k: v for k, v in summ.items() if not isinstance(v, list)}))

@@ -646,3 +646,20 @@ def test_deep_lists_split_equals_single_wave(pid, data):
         if k in split:
             assert np.array_equal(split[k], single[k], equal_nan=split[k].dtype.kind == 'f'), \
                 (k, np.flatnonzero(np.any((split[k] != single[k]).reshape(len(split[k]), -1), axis=1))[:10])
+
+
+def test_plugin_range_rows_reference_verdicts():
+    """The force-free point rejects only the fp64 range caused (tests/test_range_rows.py): on the
+    GPU, through the plugin (the device and the host steps), every row the reference decided
+    at 120 s gets its verdict -- 10 of the 12 are true solutions the device alone rejects."""
+    from problems import load_problem
+    import sympy as sp
+    rows = G.decided(G.ref_rows('ff_range_rows.jsonl'))
+    assert len(rows) >= 12
+    prob = load_problem('force_free')
+    locs = {**prob.symbols, **prob.constants, **prob.unary_ops}
+    got = prob.validator.validate_batch([sp.sympify(r['expr'], locals=locs) for r in rows],
+                                        check_regularity=False, fast_point_only=False)
+    bad = [(r['expr'], r['ok'], g) for g, r in zip(got, rows) if g[0] != r['ok']]
+    assert not bad, bad
+    assert sum(g[0] for g in got) >= 10
