@@ -47,6 +47,56 @@ def log(msg):
     print(f'[bench {time.perf_counter() - _T0:7.1f}s] {msg}', file=sys.stderr, flush=True)
 
 
+# host-measured stages before validation (recorded, not re-run by the bench): the reference's
+# enumeration + normalization of the depth-4 force-free stream on one core (SURVEY.md section 6 /
+# 8d, stream_generate), and the pre-validate filters over that whole stream on the SymPy pool
+ENUM_D4_S = 675.0
+PREFILTER_RECORD = os.path.join('profiles', 'r05_prefilter_d4.json')
+
+
+def time_to_7_end_to_end(validation_s):
+    """time_to_7_end_to_end_s: the recorded host stages plus this run's
+    validation time, labelled host-measured -- the SymPy work the north star keeps on the host."""
+    try:
+        with open(os.path.join(ROOT, PREFILTER_RECORD)) as f:
+            pf = json.load(f)
+    except OSError:
+        return {'time_to_7_end_to_end_s': None}
+    total = ENUM_D4_S + pf['wall_s'] + validation_s
+    return {'time_to_7_end_to_end_s': round(total, 1),
+            'time_to_7_end_to_end_parts': {
+                'enumeration_normalize_s': ENUM_D4_S, 'enumeration_source': 'SURVEY.md section 6 (reference, 1 core)',
+                'prefilters_s': pf['wall_s'], 'prefilters_source': f"{PREFILTER_RECORD} ({pf['procs']} SymPy processes, "
+                                                                  f"{pf['rows']} rows, kept == reference: {pf['kept_equals_reference']})",
+                'validation_s': round(validation_s, 4), 'validation_source': 'this run',
+                'label': 'host-measured recorded stages + measured validation'}}
+
+
+class heartbeat:
+    """A progress line every ``every`` seconds while a long leg runs (a leg whose work is in
+    SymPy pool processes or a C call prints nothing of its own for minutes)."""
+
+    def __init__(self, what, every=30.0):
+        import threading
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.t = threading.Thread(target=self._beat, daemon=True)
+
+    def _beat(self):
+        t0 = time.perf_counter()
+        while not self.stop.wait(self.every):
+            log(f'... {self.what}: {time.perf_counter() - t0:.0f} s')
+
+    def __enter__(self):
+        log(self.what)
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.t.join(5)
+        return False
+
+
 def load_workload(problem):
     # force-free: the depth-4 validated set; Kerr (SURVEY.md §8d C5): the whole depth<=4 stream
     # (1,024,799 candidates; the pre-validate filters keep 1,999 of a 2,000 seeded sample, so
@@ -102,6 +152,9 @@ def main():
                     help='host processes of the SymPy leg (0: OMP_NUM_THREADS, the box\'s CPU share)')
     ap.add_argument('--no-extras', action='store_true',
                     help='skip the early-exit / host-buffer / time-to-solutions legs')
+    ap.add_argument('--strict-full', action='store_true',
+                    help="only the streaming 'strict' symbolic mode over every validated d4 string "
+                         "through the worker pipeline (a steady-state rate; minutes), as one JSON line")
     ap.add_argument('--plan-only', action='store_true',
                     help='print every rank\'s environment and shard plan as JSON and exit before any GPU call')
     a = ap.parse_args()
@@ -118,6 +171,11 @@ def main():
         sys.exit(2)
     if a.plan_only:
         print(json.dumps(plan_record(a)))
+        return
+    if a.strict_full:
+        from pdeval import hostpool
+        hostpool.start()
+        print(json.dumps(strict_full()))
         return
     if not a.no_extras and int(os.environ.get('WORLD_SIZE', '1')) == 1 and a.problem == 'force_free':
         # the worker leg's SymPy pool for the strings the native compiler declines: forked now,
@@ -231,8 +289,8 @@ def main():
         if not a.no_extras and world == 1 and pid == PROBLEM_FORCE_FREE:
             # configs[4]'s operator on the same build, measured by the driver's own command:
             # the Kerr depth<=4 stream at the same per-GPU batch (the weakest kernel, pass 1)
-            log('Kerr sub-record')
-            res['kerr'] = kerr_subrecord(a.n, a.steps, a.warmup, world, rank, local, dev)
+            with heartbeat('Kerr sub-record'):
+                res['kerr'] = kerr_subrecord(a.n, a.steps, a.warmup, world, rank, local, dev)
             log('Kerr sub-record done')
 
     if not a.no_extras and world == 1:
@@ -261,6 +319,7 @@ def main():
             res['solutions'] = {k: v for k, v in rec.found.items()}
             res['solution_stream_hits'] = rec.stream_hits
             res['time_to_7_breakdown_s'] = {k: round(v, 4) for k, v in rec.seconds.items()}
+            res.update(time_to_7_end_to_end(res['time_to_7_solutions_s']))
             # the same, starting from the candidate strings instead of compiled programs: the
             # native compiler (csrc/pdcompile.cpp) plus SymPy for the strings it declines
             from pdeval import native
@@ -281,20 +340,20 @@ def main():
                 'hybrid_compile_s': round(t_comp, 4)}
 
     if not a.no_extras and world == 1 and pid == PROBLEM_FORCE_FREE:
-        log('strict-mode leg')
-        res['strict'] = strict_leg(exprs_all, local)
+        with heartbeat('strict-mode leg'):
+            res['strict'] = strict_leg(exprs_all, local)
         res['value_strict'] = res['strict']['value_strict']
         # the worker pool's batch path, queue tuples in -> result tuples out (the reference's
         # _parallel_validator_worker protocol, general_method_paper_reproduction.py:1756-1816)
-        log('worker / inline legs')
-        res['worker_process_batch'] = worker_throughput(exprs_all)
+        with heartbeat('worker / inline legs'):
+            res['worker_process_batch'] = worker_throughput(exprs_all)
 
     if rank == 0:
         if not a.no_cpu and world == 1:
             procs = a.cpu_procs or int(os.environ.get('OMP_NUM_THREADS', '0') or os.cpu_count())
             if pid == PROBLEM_FORCE_FREE:
-                log(f'SymPy CPU baseline ({a.sympy_seconds:.0f} s budget, {procs} processes)')
-                res['cpu_baseline'] = cpu_baseline_sympy(procs, a.sympy_seconds)
+                with heartbeat(f'SymPy CPU baseline ({a.sympy_seconds:.0f} s budget, {procs} processes)'):
+                    res['cpu_baseline'] = cpu_baseline_sympy(procs, a.sympy_seconds)
             log('C-oracle CPU baseline')
             res['cpu_baseline_c_port'] = cpu_baseline(pid, ops_all, off_all, idx, a.cpu_seconds)
         print(json.dumps(res))
@@ -582,7 +641,7 @@ def plan_record(a):
             'idx_head': [int(i) for i in plan.idx[:4]]}
 
 
-def strict_leg(exprs, device, n=1000, seed=0, n_stream=5000):
+def strict_leg(exprs, device, n=300, seed=0, n_stream=3000):
     """The 'strict' symbolic mode (pdeval.symbolic.suspect + the reference's symbolic stage
     replayed for the grid zeros of those shapes, 60 s per candidate over the SymPy pool):
     * batch-synchronous on a seed-0 sample of ``n`` depth-4 strings (compile, device, host
@@ -649,6 +708,52 @@ def strict_leg(exprs, device, n=1000, seed=0, n_stream=5000):
     out['value_strict'] = out['stream']['candidates_per_s'] if same and rows == len(big) else None
     out['value_strict_batch_sync'] = out['strict']['candidates_per_s']
     return out
+
+
+def strict_full(batch=4096):
+    """The streaming 'strict' mode over all 142,004 validated depth-4 strings
+    through the worker pipeline (pdeval.worker.process_batches, the default queue batch): rows at
+    device rate, suspects replayed in the SymPy pool under the 60 s bound.  Reports the whole
+    run's rate, the rate over the rows emitted before the last batch left the device (the
+    steady state, before the tail of replays still in the pool), the suspect fraction and the
+    timeouts, and whether the final tuples equal the default mode's except on replayed rows."""
+    from pdeval.workload import load_programs
+    from problems import load_problem
+    from problems.force_free.validator import PreciseFoliationValidator
+    from pdeval.worker import KnownSolutionTagger, filtered_kwargs, process_batches
+    _, _, exprs = load_programs('force_free_d4_validated.npz')
+    strs = [str(e) for e in exprs]
+    prob = load_problem('force_free')
+    locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
+    tagger = KnownSolutionTagger(prob, locs)
+    items = [(i + 1, x) for i, x in enumerate(strs)]
+    v = PreciseFoliationValidator(symbolic='strict')
+    kw = filtered_kwargs(prob.validator)
+    stats, got, marks = {}, [], []
+    with heartbeat(f"streaming strict mode over {len(items)} strings"):
+        t0 = time.perf_counter()
+        for r in process_batches((items[k:k + batch] for k in range(0, len(items), batch)), v, kw, locs, tagger,
+                                 stats=stats):
+            got.extend(r)
+            marks.append((time.perf_counter() - t0, len(got)))
+        dt = time.perf_counter() - t0
+    # the default mode's tuples of the same stream, for the comparison
+    off = {t[5]: t for r in process_batches((items[k:k + batch] for k in range(0, len(items), batch)),
+                                            prob.validator, kw, locs, tagger) for t in r}
+    by = {t[5]: t for t in got}
+    changed = sorted(i for i in by if by[i][1] != off[i][1])
+    # steady state: the rows out by the time the device stream ended (the first mark at which
+    # every batch's ready rows are out), over that time
+    n_ready = len(items) - stats.get('sent', 0)
+    t_ready = next((t for t, k in marks if k >= n_ready), dt)
+    return {'metric': "strict-mode candidates/s (force-free depth-4, worker pipeline, streaming)",
+            'strings': len(items), 'rows': len(got), 'complete': sorted(by) == list(range(1, len(items) + 1)),
+            'seconds': round(dt, 2), 'candidates_per_s': round(len(items) / dt, 1),
+            'steady_state_candidates_per_s': round(n_ready / t_ready, 1), 'ready_rows_out_s': round(t_ready, 2),
+            **stats, 'suspect_fraction': round(stats.get('suspect', 0) / len(items), 5),
+            'suspect_fraction_of_grid_zeros': round(stats.get('suspect', 0) / max(1, stats.get('grid_zero', 0)), 4),
+            'verdicts_changed_vs_default': len(changed), 'changed_rows_sample': [by[i][5] for i in changed[:20]],
+            'batch': batch, 'timeout_s': v.symbolic_timeout}
 
 
 def worker_throughput(exprs, batch=4096, pipe_batch=32768, inline_n=2000):

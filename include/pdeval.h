@@ -173,8 +173,18 @@ typedef struct pdeval_outputs {
     double*  q_ref;          /* n, scaled residual at the point stage (Kerr: max |lhs|)    */
     double*  res_ref;        /* n * n_ref, raw residual at each reference point (complex:
                                 its modulus with the sign of its real part)              */
-    double*  q_grid;         /* n, max scaled residual over the finite grid points         */
-    int32_t* n_bad;          /* n, grid points with q > tau_grid                           */
+    double*  q_grid;         /* n, max scaled residual q = |res| / S over the finite grid
+                                points.  Kerr: the IEEE quotient of the point with the largest
+                                estimate (its grid-reject text prints it).  Force-free: the
+                                maximum of the estimates |res| * rcp(S) themselves (hardware
+                                reciprocal, ~1 ulp; no reason text reads it), so a diagnostic  */
+    int32_t* n_bad;          /* n, grid points that fail the zero test |res| > tau_grid * S
+                                (no division; equal to q > tau_grid except within a rounding
+                                of tau_grid); after tier 2, only points whose residual also
+                                exceeds its rounding-noise bound.  Tier 2 re-checks the 64-point
+                                chunks where tier 1 failed a point (ESC_MASK): a point tier 1
+                                passed is the same comparison on the same values and is not
+                                re-counted                                                  */
     int32_t* n_nonfinite;    /* n, grid points where the evaluation was not finite         */
     double*  fingerprint;    /* n * PDEVAL_FP_N, u at fixed points (known-solution tags)   */
 } pdeval_outputs;

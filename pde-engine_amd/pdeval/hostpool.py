@@ -122,9 +122,14 @@ def _call_on_thread(fn, x, item_timeout, default):
     return v
 
 
-def _child(tasks, results):
+_CANCEL_SLOTS = 4096    # ring of per-job cancel flags shared with the children (job % slots)
+
+
+def _child(tasks, results, cancelled=None):
     # children: SymPy only (no GPU, no threads of their own); the SymPy side is imported here,
-    # once per child, not inside the first batch that reaches it
+    # once per child, not inside the first batch that reaches it.  A job the parent gave up on
+    # (its deadline passed) is flagged in ``cancelled``: its chunks still queued are answered
+    # with the default at once instead of running ahead of the next jobs.
     os.environ['OMP_NUM_THREADS'] = '1'
     signal.signal(signal.SIGINT, signal.SIG_IGN)
     from . import problem_defs   # noqa: F401  (sympy, the flattener, the problems' locals)
@@ -137,6 +142,9 @@ def _child(tasks, results):
         try:
             out = []
             for x in items:
+                if cancelled is not None and cancelled[job % _CANCEL_SLOTS]:
+                    out.append(default)
+                    continue
                 try:
                     out.append(_call_bounded(fn, x, item_timeout, default))
                 except _ItemTimeout:     # (a late timer: the item counts as timed out)
@@ -155,7 +163,8 @@ class _FixedPool:
         self.n = n
         self.tasks = ctx.Queue()
         self.results = ctx.Queue()
-        self.procs = [ctx.Process(target=_child, args=(self.tasks, self.results), daemon=True)
+        self.cancelled = ctx.RawArray('b', _CANCEL_SLOTS)
+        self.procs = [ctx.Process(target=_child, args=(self.tasks, self.results, self.cancelled), daemon=True)
                       for _ in range(n)]
         for p in self.procs:
             p.start()
@@ -197,6 +206,8 @@ class _FixedPool:
         with self.lock:
             late = [j for j, (_f, dl, _d) in self.futures.items() if dl is not None and now > dl]
             got = [self.futures.pop(j) for j in late]
+        for j in late:
+            self.cancelled[j % _CANCEL_SLOTS] = 1
         for f, _dl, d in got:
             if not f.done():
                 self.overdue += 1
@@ -214,6 +225,7 @@ class _FixedPool:
                 return fut
             self.job += 1
             job = self.job
+            self.cancelled[job % _CANCEL_SLOTS] = 0
             dl = None
             if item_timeout:
                 ahead = len(self.futures) + 1
@@ -239,6 +251,7 @@ class _FixedPool:
                 return [None] * len(chunks)
             self.job += 1
             job = self.job
+            self.cancelled[job % _CANCEL_SLOTS] = 0
             box = self.inbox[job] = _queue.Queue()
         try:
             for k, ch in enumerate(chunks):
@@ -252,6 +265,8 @@ class _FixedPool:
                         break
                     if deadline is not None and time.monotonic() > deadline:
                         self.overdue += 1
+                        # its chunks still queued yield the default in the children at once
+                        self.cancelled[job % _CANCEL_SLOTS] = 1
                         return [got[k] if k in got else [default] * len(chunks[k]) for k in range(len(chunks))]
                     continue
                 got[k] = out if ok else None

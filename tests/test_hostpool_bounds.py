@@ -141,3 +141,38 @@ def test_pool_job_deadline_stuck_child():
             "import test_hostpool_bounds as t; t._pool_deadline_body(); print('BODY-OK')")
     p = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0 and 'BODY-OK' in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
+
+
+def _sleep_unsignalled(x):
+    """'hang4' sleeps 4 s and 's1' 1 s, with SIGALRM blocked (no per-item bound reaches them)."""
+    signal.pthread_sigmask(signal.SIG_BLOCK, {signal.SIGALRM})
+    try:
+        time.sleep({'hang4': 4.0, 's1': 1.0}.get(x, 0.0))
+    finally:
+        signal.pthread_sigmask(signal.SIG_UNBLOCK, {signal.SIGALRM})
+    return x
+
+
+def _pool_cancel_body():
+    from pdeval import hostpool
+    hostpool.DEADLINE_MARGIN_S = 0.5
+    assert hostpool.start(1) is not None
+    try:
+        got = hostpool.run(_sleep_unsignalled, ['hang4'] + ['s1'] * 5, min_items=1, item_timeout=0.2, default='T')
+        assert got == ['T'] * 6 and hostpool._POOL.overdue == 1, got
+        # the overdue job's items still queued are skipped once the child is free again: the
+        # next job waits for the 4 s hang only, not for five more 1 s items
+        t0 = time.time()
+        assert hostpool.run(_sleep_unsignalled, ['y'], min_items=1) == ['y']
+        assert time.time() - t0 < 3.5, time.time() - t0
+    finally:
+        hostpool.stop()
+
+
+def test_pool_overdue_job_is_cancelled():
+    """after a job's deadline its unfinished chunks no longer run ahead of the next
+    jobs (a shared per-job cancel flag the children check before each item)."""
+    code = (f"import sys; sys.path[:0] = [{HERE!r}, {os.path.join(os.path.dirname(HERE), 'pde-engine_amd')!r}]; "
+            "import test_hostpool_bounds as t; t._pool_cancel_body(); print('BODY-OK')")
+    p = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and 'BODY-OK' in p.stdout, (p.stdout[-2000:], p.stderr[-4000:])
