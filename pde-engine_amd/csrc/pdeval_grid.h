@@ -1216,8 +1216,8 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                 if constexpr (PD_DIVFREE) {
                     gm.add(r.finite, r.res_abs, r.scale);
                     grad_nz = grad_nz | (r.finite & !r.grad_zero);
-                    nfin += count_lanes(r.finite);
-                    const uint64_t fm = lane_mask(r.finite & grid_fails(r.res_abs, r.scale, a.prm.tau_grid));
+                    nfin += (int)__popcll(r.fin_lanes);
+                    const uint64_t fm = r.fin_lanes & lane_mask(grid_fails(r.res_abs, r.scale, a.prm.tau_grid));
                     nbad += (int)__popcll(fm);
                     // the chunk's failing lanes, for tier 2 (a candidate the point stage rejected
                     // is final and never escalates)

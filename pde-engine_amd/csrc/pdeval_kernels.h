@@ -638,7 +638,26 @@ struct PointResult {
     double scale;           // S
     bool grad_zero;         // u_x == u_y == 0 exactly
     bool finite;
+    uint64_t fin_lanes;     // the wave's lanes where `finite` holds (grid passes; PD_BALLOT_SPLIT)
 };
+// The grid passes count finite points with a ballot of `finite`.  `finite` is an AND of several
+// compares, and a ballot of such an AND is lowered as a select of 0/1 into a VGPR and a compare
+// of it (2 VALU per ballot, twice per point); a ballot of one compare is the compare's own lane
+// mask.  So the lean epilogues form fin_lanes as the AND of the ballots of the individual
+// compares (the same lanes), and grid_body ballots only the zero test's compare beside it.
+#ifndef PD_BALLOT_SPLIT
+#define PD_BALLOT_SPLIT 1
+#endif
+// isfinite as a plain compare (|x| <= DBL_MAX: false for an infinity and for NaN), so that its
+// ballot folds: isfinite itself lowers to v_cmp_class, which the ballot combine does not match
+__device__ __forceinline__ bool finite_cmp(double x) { return fabs(x) <= 0x1.fffffffffffffp+1023; }
+__device__ __forceinline__ uint64_t ballot64(bool b) {
+#ifndef PD_HOST_SIM
+    return __builtin_amdgcn_ballot_w64(b);
+#else
+    return __ballot(b);
+#endif
+}
 
 // Force-free foliation determinant from the order-4 jet of u.
 // p = u_rho, q = u_z (order 3);  A = p_rho + q_z - p/rho,  B = p^2 + q^2 (order 2);
@@ -875,12 +894,19 @@ template <class T> __device__ __forceinline__ PointResult ff_epilogue_p(const T*
         const double* c = reinterpret_cast<const double*>(u);
         double m = max_abs(max_abs(max_abs(c[1], c[2]), max_abs(c[3], c[4])), max_abs(max_abs(c[5], c[6]), max_abs(c[7], c[8])));
         m = max_abs(m, max_abs(max_abs(max_abs(c[9], c[10]), max_abs(c[11], c[12])), max_abs(c[13], c[14])));
+        const double d0 = *reinterpret_cast<const double*>(&det);
+        if constexpr (PD_BALLOT_SPLIT)
+            r.fin_lanes = ballot64(finite_cmp(d0)) & ballot64(finite_cmp(S)) & ballot64(m < kHugeJet) & ballot64(jet_coef_ok(c[0]));
         fin = fin & (m < kHugeJet) & jet_coef_ok(u[0]);
+        r.finite = fin;
+        if constexpr (!PD_BALLOT_SPLIT) r.fin_lanes = ballot64(fin);
+        return r;
     } else {
 #pragma unroll
         for (int i = 0; i < 15; ++i) fin = fin & jet_coef_ok(u[i]);
     }
     r.finite = fin;
+    r.fin_lanes = ballot64(fin);
     return r;
 }
 
@@ -913,7 +939,7 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue(const T*
     }
     r.grad_zero = is_zero(u[ji(1, 0)]) && is_zero(u[ji(0, 1)]);
     bool fin = finite_(L) && isfinite(r.scale);
-    // a jet that is exactly 0 to second order carries no information: u underflowed there
+    // (fin_lanes below) a jet that is exactly 0 to second order carries no information: u underflowed there
     // (exp_neg(E*exp(r**2)*..) is 0 in fp64 on most of the grid), as an analytic u that is not
     // identically 0 cannot vanish with its derivatives at a sample point
     // (u_rx, coefficient ji(1, 1), is not in the operator -- no mixed term, kerr validator.py
@@ -926,6 +952,7 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue(const T*
         allz = allz && is_zero(u[i]);
     }
     r.finite = fin && !allz;
+    r.fin_lanes = ballot64(r.finite);
     return r;
 }
 
@@ -967,6 +994,10 @@ template <class T> __device__ __forceinline__ PointResult kerr_epilogue_lean(con
                              u[ji(0, 2)]);
     // (bitwise: && would make the compiler branch around the later tests)
     r.finite = isfinite(r.scale) & !isnan(u[ji(0, 0)]) & (m < kHugeJet) & (m != 0.0);
+    if constexpr (PD_BALLOT_SPLIT)
+        r.fin_lanes = ballot64(finite_cmp(r.scale)) & ballot64(u[ji(0, 0)] == u[ji(0, 0)]) & ballot64(m < kHugeJet) & ballot64(m != 0.0);
+    else
+        r.fin_lanes = ballot64(r.finite);
     return r;
 }
 
