@@ -155,6 +155,8 @@ def main():
     ap.add_argument('--strict-full', action='store_true',
                     help="only the streaming 'strict' symbolic mode over every validated d4 string "
                          "through the worker pipeline (a steady-state rate; minutes), as one JSON line")
+    ap.add_argument('--part', type=int, default=0, help='--strict-full: this share of the set')
+    ap.add_argument('--parts', type=int, default=1, help='--strict-full: shares of the set')
     ap.add_argument('--plan-only', action='store_true',
                     help='print every rank\'s environment and shard plan as JSON and exit before any GPU call')
     a = ap.parse_args()
@@ -175,7 +177,7 @@ def main():
     if a.strict_full:
         from pdeval import hostpool
         hostpool.start()
-        print(json.dumps(strict_full()))
+        print(json.dumps(strict_full(part=a.part, parts=a.parts)))
         return
     if not a.no_extras and int(os.environ.get('WORLD_SIZE', '1')) == 1 and a.problem == 'force_free':
         # the worker leg's SymPy pool for the strings the native compiler declines: forked now,
@@ -703,7 +705,7 @@ def strict_leg(exprs, device, n=300, seed=0, n_stream=2000):
     return out
 
 
-def strict_full(batch=4096):
+def strict_full(batch=4096, part=0, parts=1):
     """The streaming 'strict' mode over all 142,004 validated depth-4 strings
     through the worker pipeline (pdeval.worker.process_batches, the default queue batch): rows at
     device rate, suspects replayed in the SymPy pool under the 60 s bound.  Reports the whole
@@ -716,10 +718,13 @@ def strict_full(batch=4096):
     from pdeval.worker import KnownSolutionTagger, filtered_kwargs, process_batches
     _, _, exprs = load_programs('force_free_d4_validated.npz')
     strs = [str(e) for e in exprs]
+    # --parts: a contiguous share of the set per call (one GPU call is bounded in time); the
+    # parts' rows and seconds add up to the whole set's rate
+    lo, hi = len(strs) * part // parts, len(strs) * (part + 1) // parts
     prob = load_problem('force_free')
     locs = {**prob.unary_ops, **prob.symbols, **prob.constants}
     tagger = KnownSolutionTagger(prob, locs)
-    items = [(i + 1, x) for i, x in enumerate(strs)]
+    items = [(i + 1, x) for i, x in enumerate(strs)][lo:hi]
     v = PreciseFoliationValidator(symbolic='strict')
     kw = filtered_kwargs(prob.validator)
     stats, got, marks = {}, [], []
@@ -735,17 +740,19 @@ def strict_full(batch=4096):
                                             prob.validator, kw, locs, tagger) for t in r}
     by = {t[5]: t for t in got}
     changed = sorted(i for i in by if by[i][1] != off[i][1])
+    ids = [i for i, _ in items]
     # steady state: the rows out by the time the device stream ended (the first mark at which
     # every batch's ready rows are out), over that time
     n_ready = len(items) - stats.get('sent', 0)
     t_ready = next((t for t, k in marks if k >= n_ready), dt)
     return {'metric': "strict-mode candidates/s (force-free depth-4, worker pipeline, streaming)",
-            'strings': len(items), 'rows': len(got), 'complete': sorted(by) == list(range(1, len(items) + 1)),
+            'part': part, 'parts': parts, 'rows_range': [lo, hi],
+            'strings': len(items), 'rows': len(got), 'complete': sorted(by) == ids,
             'seconds': round(dt, 2), 'candidates_per_s': round(len(items) / dt, 1),
             'steady_state_candidates_per_s': round(n_ready / t_ready, 1), 'ready_rows_out_s': round(t_ready, 2),
             **stats, 'suspect_fraction': round(stats.get('suspect', 0) / len(items), 5),
             'suspect_fraction_of_grid_zeros': round(stats.get('suspect', 0) / max(1, stats.get('grid_zero', 0)), 4),
-            'verdicts_changed_vs_default': len(changed), 'changed_rows_sample': [by[i][5] for i in changed[:20]],
+            'verdicts_changed_vs_default': len(changed), 'changed_rows_sample': [dict(items)[i] for i in changed[:20]],
             'batch': batch, 'timeout_s': v.symbolic_timeout}
 
 

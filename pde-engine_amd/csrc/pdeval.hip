@@ -589,54 +589,76 @@ extern "C" int pdeval_program_depth(const int32_t* ops, int64_t n_words) {
     return dmax;
 }
 
-// Algorithmic FP64 flop model per sample point (DESIGN.md "Roofline"): jet work of each
-// opcode at the problem's order plus the residual epilogue.
-// Force-free needs every coefficient of the order-4 jets (15); Kerr's operator only u, u_r,
-// u_x, u_rr, u_xx -- 5 of the 6 order-2 coefficients (no mixed term, kerr validator.py:77-91),
-// and the mixed one feeds nothing else, so it is not counted (nor computed by the lean passes).
-// Products: coefficient (i, j) of a jet product takes (i+1)(j+1) of them, so a full product is
-// 70 for K = 4 (2*70 - 15 = 125 flops) and 11 for Kerr's 5 coefficients (2*11 - 5 = 17).
-// FP64 flops of one opcode at one sample point (the model of pdeval_program_flops)
-static double op_flops(bool ff, uint32_t w) {
-    const int K = ff ? 4 : 2;
-    const double NC = ff ? 15.0 : 5.0;
-    const double mulf = ff ? 125.0 : 17.0;
-    const double divf = mulf + NC + 10.0;
-    // Horner composition: sum over levels (2*#products) + coefficient chain (Kerr: the level
-    // products of h (h_00 = 0) into the 5 coefficients, 6 + 2)
-    const double compf = ff ? (2.0 * 91.0 + 3.0 * K) : (2.0 * 8.0 + 3.0 * K);
-    switch (w & 0xffu) {
-        case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: return NC;
-        case PDOP_MUL: return mulf;
-        case PDOP_DIV: case PDOP_RDIV: case PDOP_RDIVC: return divf;
-        case PDOP_ADDC: case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: return 2;
-        case PDOP_MULC: case PDOP_NEG: case PDOP_ABS: return NC;
-        case PDOP_MUL_X: case PDOP_MUL_Y: case PDOP_DIV_X: case PDOP_DIV_Y: return 2 * NC;
+// FP64 flop model per sample point (DESIGN.md section 7 "Roofline"): the FP64 operations the lean
+// grid pass executes for each opcode at one point, plus the residual epilogue -- measured once per
+// problem on the calibration programs (scripts/microbench.py --set calib under PMC, fitted by
+// scripts/flop_calib.py: FLOPs = 2 FMA + MUL + ADD per lane, TRANS estimates not counted;
+// profiles/r06_c_calib_force_free.json, profiles/r06_g_calib_kerr_magnetosphere.json), so that the
+// model and the SQ counters of a whole batch agree (the round-5 algorithmic
+// table was 8 % above the counters for force-free and 7 % below for Kerr).  Where the kernel does
+// more than the textbook jet operation, the table says so: a quotient coefficient is a
+// Markstein-corrected division (a/a == 1 exactly), a division by a coordinate divides every
+// coefficient; a coordinate push reads the power tables (no arithmetic); NEG is folded into the
+// tracked sign by the decoder (PD_FOLD_NEG).  Force-free order 4 (15 coefficients); Kerr's 5 live
+// coefficients of order 2 (no mixed term, kerr validator.py:77-91).
+struct OpCost {
+    double add, mul, sq, div, addc, mulc, var, divvar, exp, log, sqrt, pow, padd, pmul, pdiv, prdiv, fused_var,
+        fused_p, epi;
+};
+// force-free: r06_c calibration, POWN from r06_h (n = 2: 66, 3: 193, 4: 132, 5: 501, 7: 751 -- the
+// square and product costs below); Kerr: r06_g (the fused PUSH_C + MUL_X / MUL_Y / MUL_P of the
+// decoder, pdeval_grid.h decode_kernel: c times the coordinate, or c times K + 1 power coefficients)
+static constexpr OpCost kCostFF = {15.0, 125.0, 66.0, 198.0, 1.0, 15.0, 25.0, 85.0, 181.0, 248.0, 188.0, 220.0,
+                                   5.5, 66.0, 75.0, 198.0, 25.0, 66.0, 244.0};
+static constexpr OpCost kCostKerr = {5.0, 18.0, 11.5, 50.0, 2.5, 6.5, 5.0, 26.0, 41.0, 104.5, 43.5, 57.0,
+                                     7.0, 13.5, 26.0, 50.0, 2.0, 3.0, 15.3};
+// prev: the opcode before w (Kerr's decoder fuses PUSH_C with a following MUL_X / MUL_Y / MUL_P)
+static double op_flops(bool ff, uint32_t w, uint32_t prev = 0xffu) {
+    const OpCost& k = ff ? kCostFF : kCostKerr;
+    const uint32_t op = w & 0xffu;
+    if (!ff && (prev & 0xffu) == PDOP_PUSH_C) {
+        if (op == PDOP_MUL_X || op == PDOP_MUL_Y) return k.fused_var;
+        if (op == PDOP_MUL_P) return k.fused_p;
+    }
+    switch (op) {
+        case PDOP_ADD: case PDOP_SUB: case PDOP_RSUB: return k.add;
+        case PDOP_MUL: return k.mul;
+        case PDOP_DIV: case PDOP_RDIV: case PDOP_RDIVC: return k.div;
+        case PDOP_ADDC: case PDOP_ADD_X: case PDOP_ADD_Y: case PDOP_SUB_X: case PDOP_SUB_Y: return k.addc;
+        case PDOP_MULC: case PDOP_ABS: return k.mulc;
+        case PDOP_NEG: return 0.0;
+        case PDOP_MUL_X: case PDOP_MUL_Y: return k.var;
+        case PDOP_DIV_X: case PDOP_DIV_Y: return k.divvar;
         case PDOP_POWN: {
-            int n = (w >> 8) & 0xff, m = 0;
-            while (n > 1) { m += 1 + (n & 1); n >>= 1; }
-            return m * mulf;
+            // pdeval_grid.h Lean::pown_lean: n = 2 a square, 3 a square and a product, 4 two
+            // squares, 5..8 n - 1 products
+            const int n = (w >> 8) & 0xff;
+            return n == 2 ? k.sq : n == 3 ? k.sq + k.mul : n == 4 ? 2.0 * k.sq : (n - 1) * k.mul;
         }
-        case PDOP_POW: case PDOP_SQRT: case PDOP_EXP: case PDOP_LOG: return compf;
-        // coordinate powers: K+1 coefficients, then a sparse (univariate) product/quotient
-        case PDOP_PUSH_P: return 3 * (K + 1);
-        case PDOP_ADD_P: case PDOP_SUB_P: return 4 * (K + 1);
-        case PDOP_MUL_P: return 3 * (K + 1) + (ff ? 50.0 : 11.0);
-        case PDOP_DIV_P: return 3 * (K + 1) + (ff ? 60.0 : 15.0);
-        case PDOP_RDIV_P: return 3 * (K + 1) + divf;
-        default: return 0.0;
+        case PDOP_EXP: return k.exp;
+        case PDOP_LOG: return k.log;
+        case PDOP_SQRT: return k.sqrt;
+        case PDOP_POW: return k.pow;
+        case PDOP_ADD_P: case PDOP_SUB_P: return k.padd;
+        case PDOP_MUL_P: return k.pmul;
+        case PDOP_DIV_P: return k.pdiv;
+        case PDOP_RDIV_P: return k.prdiv;
+        default: return 0.0;   // pushes: the jet of a coordinate, a constant or a power table entry
     }
 }
 
 extern "C" double pdeval_program_flops(int problem_id, const int32_t* ops, int64_t n_words) {
     const bool ff = problem_id == PDEVAL_PROBLEM_FORCE_FREE;
     double f = 0.0;
+    uint32_t prev = 0xffu;
     for (int64_t pc = 1; pc < n_words;) {
-        f += op_flops(ff, (uint32_t)ops[pc]);
+        f += op_flops(ff, (uint32_t)ops[pc], prev);
+        prev = (uint32_t)ops[pc];
         pc += op_words(ops[pc]);
     }
-    // epilogue: force-free determinant + its magnitude shadow; Kerr 4-term operator + scale
-    f += ff ? 2.0 * 160.0 : 16.0;
+    // epilogue: force-free determinant + its magnitude shadow + the zero test; Kerr's 4-term
+    // operator + scale + the zero test
+    f += (ff ? kCostFF : kCostKerr).epi;
     return f;
 }
 
@@ -685,7 +707,7 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
                 ++d;
                 msk[d] = (op2 == PDOP_MUL_Y || (op2 == PDOP_MUL_P && ((w2 >> 16) & 1u))) ? 2u : 1u;
                 if (d == 2) { seg_start = pc; seg_nh = 0; seg_f0 = f; }
-                f += op_flops(ff, w) + op_flops(ff, w2);
+                f += op_flops(ff, w) + op_flops(ff, w2, w);
                 pc += len + 1;
                 track_prefix(pc);
                 continue;
@@ -724,7 +746,7 @@ extern "C" double pdeval_program_hoist_flops(int problem_id, const int32_t* ops,
         pc += len;
         track_prefix(pc);
     }
-    // (a NEG the decoder folds away is charged like any opcode: the model folds none; force-free
+    // (a NEG costs nothing in the model -- the decoder folds it into the tracked sign; force-free
     // hoists prefixes of x only, pdeval_grid.h)
     double h = 0.0;
     int64_t hp = 0;

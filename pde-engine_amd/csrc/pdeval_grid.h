@@ -483,6 +483,9 @@ template <int W> struct PowTab {
 #ifndef PD_FAST_SCALED
 #define PD_FAST_SCALED 0
 #endif
+#ifndef PD_LEAN_PTR
+#define PD_LEAN_PTR 1
+#endif
 template <class T, int K, int W, int MAXD> struct Lean {
     using O = JetOps<T, K>;
     using J = typename O::J;
@@ -566,6 +569,9 @@ template <class T, int K, int W, int MAXD> struct Lean {
         // LDS -- two LDS slots of W = 2 Kerr jets (12 KiB per wave) held pass 2 at ~3 waves
         // per SIMD; with one, VGPRs set the occupancy
         J reg[RSLOT ? W : 1];
+        // (PD_LEAN_PTR) the position as a pointer: the next word's address is one 64-bit add of
+        // the scaled distance, not a sign extension, a shift and an add of an index per opcode
+        const int32_t* cur = dec + pc0;
         int pc = pc0;
         // an opcode word and the two after it (its f64 immediate, when it has one) are read
         // together, one op ahead, so an op's immediate is in SGPRs when its turn comes instead
@@ -594,8 +600,9 @@ template <class T, int K, int W, int MAXD> struct Lean {
 #else
             const int pn_at = npc;
 #endif
-            const uint32_t wn = rd_word(dec + pn_at);
-            const double immn = PD_LEAN_IMM_PREFETCH ? rd_imm(dec + pn_at + 1) : 0.0;
+            const int32_t* nxt = PD_LEAN_PTR && !PD_PREFETCH_SELECT ? cur + ((w >> DEC_DIST) & DEC_DIST_MAX) : dec + pn_at;
+            const uint32_t wn = rd_word(nxt);
+            const double immn = PD_LEAN_IMM_PREFETCH ? rd_imm(nxt + 1) : 0.0;
             const double cimm = PD_LEAN_IMM_PREFETCH ? imm : rd_imm(dec + pc + 1);
             const int pn = (int)((w >> 8) & 0xffu);   // POWN exponent / coordinate power n
             const bool on_y = (w >> 16) & 1u;         // coordinate-power axis
@@ -779,6 +786,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
             if (!more || (PRE && npc == stop)) break;
             first = false;
             pc = npc;
+            cur = nxt;
             w = wn;
             imm = immn;
         }
@@ -1221,9 +1229,11 @@ __device__ __forceinline__ void grid_body(const KernelArgs& a, int64_t cand, int
                     nbad += (int)__popcll(fm);
                     // the chunk's failing lanes, for tier 2 (a candidate the point stage rejected
                     // is final and never escalates)
-                    if (a.fmask && (ps & 3) != P0_REJECT && lane == 0) {
+                    if (a.fmask && (ps & 3) != P0_REJECT) {
                         const int ch = (row + q) * per_row + sl;
-                        if (!fsparse || fm) a.fmask[cand * (int64_t)(a.nx * per_row) + ch] = fm;
+                        if (lane == 0 && (!fsparse || fm)) a.fmask[cand * (int64_t)(a.nx * per_row) + ch] = fm;
+                        // (outside lane 0's branch: the bitmap stays wave-uniform, in SGPRs -- in
+                        // the branch it was a VGPR pair spilled to scratch and reloaded per point)
                         if (fm) fsum |= 1ull << (ch & 63);
                     }
                 } else {

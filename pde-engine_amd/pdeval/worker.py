@@ -380,8 +380,8 @@ class StrictStream:
         return out
 
 
-def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, compilers: int = 4,
-                    stream_strict: bool = True, stats: Optional[dict] = None):
+def process_batches(batches, validator, kwargs, locs, tagger, depth: Optional[int] = None,
+                    compilers: Optional[int] = None, stream_strict: bool = True, stats: Optional[dict] = None):
     """process_batch over an iterable of claimed batches, pipelined in four stages on their own
     threads: the next batches compile on the host (``compilers`` threads, so that one batch's
     native compile -- C++ threads, GIL released -- overlaps another's wait for the SymPy pool),
@@ -406,6 +406,11 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: int = 8, co
         return
     from collections import deque
     from concurrent.futures import ThreadPoolExecutor
+    # (defaults 8 batches in flight and 4 compile threads; PDEVAL_PIPE_DEPTH / _COMPILERS)
+    if depth is None:
+        depth = int(os.environ.get('PDEVAL_PIPE_DEPTH', '8'))
+    if compilers is None:
+        compilers = int(os.environ.get('PDEVAL_PIPE_COMPILERS', '4'))
     bv = validator._validator()
     sym = _symbolic_args(validator)
     strict = None

@@ -28,12 +28,16 @@ CALIB_FF = ['rho', 'z', 'rho*z', 'rho + z', 'rho - z', '3*rho*z', 'rho*z + 3', '
             'exp(rho*z)', 'sqrt(rho*z + 7)', 'log(rho*z + 7)', '(rho*z + 7)**(3/2)', '(rho*z + 7)**(-3/2)',
             '(rho*z + 7)**(1/4)', '(rho*z)**2', '(rho*z)**3', '(rho*z)**4', '(rho*z)**5', '(rho*z)**7',
             'rho**2*z', 'rho + z**2', 'rho*z + rho**2', 'rho*z - rho**3', 'rho*z/rho**2', 'rho**2/(rho*z + 7)',
-            'rho**3*z**2', 'Abs(rho*z - 1)', '3/(rho*z + 7)', 'z*rho + z**2']
+            'rho**3*z**2', 'Abs(rho*z - 1)', '3/(rho*z + 7)', 'z*rho + z**2',
+            '(rho*z + 7)**2', '(rho*z + 7)**3', '(rho*z + 7)**4', '(rho*z + 7)**5', '(rho*z + 7)**7',
+            'z/(rho*z + 7)', 'rho**2*z + rho*z']
 CALIB_KERR = ['r', 'x', 'r*x', 'r + x', 'r - x', '3*r*x', 'r*x + 3', 'r/x', 'x/r', '(r + x)*(r - x)',
               '(r + x)/(r - x + 7)', '(r + x) - (r*x + 7)', 'exp(r*x)', 'sqrt(r*x + 7)', 'log(r*x + 7)',
               '(r*x + 7)**(3/2)', '(r*x + 7)**(-3/2)', '(r*x + 7)**(1/4)', '(r*x)**2', '(r*x)**3', '(r*x)**4',
               '(r*x)**5', '(r*x)**7', 'r**2*x', 'r + x**2', 'r*x + r**2', 'r*x - r**3', 'r*x/r**2',
-              'r**2/(r*x + 7)', 'r**3*x**2', 'Abs(r*x - 1)', '3/(r*x + 7)', 'x*r + x**2', 'M*r*x', 'a*r*x']
+              'r**2/(r*x + 7)', 'r**3*x**2', 'Abs(r*x - 1)', '3/(r*x + 7)', 'x*r + x**2', 'M*r*x', 'a*r*x',
+              '(r*x + 7)**2', '(r*x + 7)**3', '(r*x + 7)**4', '(r*x + 7)**5', '(r*x + 7)**7',
+              'x/(r*x + 7)', 'r**2*x + r*x']
 
 
 def programs(problem_id: int, which: str):

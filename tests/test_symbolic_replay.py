@@ -174,8 +174,11 @@ def test_strict_mode_every_decided_row():
     strs = [r['expr'] for r in rows]
     ops, off, _ = P.compile_strings(pd, strs)
     ora = O.validate_mt(0, ops, off)
-    from pdeval.batch import symbolic_zero_gradient
-    symbolic_zero_gradient(pd, strs, ora)           # (the host step every result goes through)
+    from pdeval.batch import ff_range_point_check, symbolic_zero_gradient
+    # (the host steps every result goes through: the fp64-range point rejects, then the
+    # zero-gradient check -- pdeval.batch.apply_host_steps, default params: full grid, max_bad 0)
+    ff_range_point_check(pd, strs, ora, ops, off, 4096, True, 0)
+    symbolic_zero_gradient(pd, strs, ora)
     rep = _replay_rows()
     zero = np.isin(ora['status'], (CLS_ACCEPT, CLS_REJECT_SYMBOLIC))
     n_suspect = n_timeout = 0
