@@ -89,6 +89,9 @@ struct pdeval_ctx {
     int list_queue = PD_LIST_QUEUE;   // list passes: 0 static schedule, k > 0 queue chunks of k items
     int list_parts = PD_LIST_PARTS;   // list passes: waves per candidate at full size
     uint8_t* d_ddps = nullptr;      // the early tier's classes, capacity cap
+    double* d_dd_res = nullptr;     // speculative provisional passes' outputs (cap * 4, cap)
+    double* d_dd_q = nullptr;
+    bool dd_spec = true;            // env PDEVAL_DD_SPEC=0: provisional passes after the grid (A/B)
     double ref_x[4] = {0, 0, 0, 0}, ref_y[4] = {0, 0, 0, 0};
     dd ref_xd[4] = {}, ref_yd[4] = {};   // the reference points as double-doubles
     dd kc_ref[16] = {};                  // Kerr operator coefficients there, double-double
@@ -444,6 +447,7 @@ extern "C" int pdeval_create(int device_id, int problem_id, const double* grid, 
     if (const char* v = getenv("PDEVAL_LEAN_CPLX")) c->lean_cplx = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_GRAPH")) c->use_graph = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_DD_EARLY")) c->dd_early = atoi(v) != 0;
+    if (const char* v = getenv("PDEVAL_DD_SPEC")) c->dd_spec = atoi(v) != 0;
     if (const char* v = getenv("PDEVAL_LIST_QUEUE")) c->list_queue = std::max(0, atoi(v));
     if (const char* v = getenv("PDEVAL_LIST_PARTS")) c->list_parts = std::min(16, std::max(1, atoi(v)));
     if (const char* v = getenv("PDEVAL_HOIST")) c->hoist = atoi(v) != 0;
@@ -485,6 +489,8 @@ extern "C" int pdeval_destroy(pdeval_ctx* c) {
         if (l) (void)hipFree(l);
     if (c->d_pstate) (void)hipFree(c->d_pstate);
     if (c->d_ddps) (void)hipFree(c->d_ddps);
+    if (c->d_dd_res) (void)hipFree(c->d_dd_res);
+    if (c->d_dd_q) (void)hipFree(c->d_dd_q);
     if (c->d_dec) (void)hipFree(c->d_dec);
     if (c->d_hoist) (void)hipFree(c->d_hoist);
     if (c->d_hoist_own) (void)hipFree(c->d_hoist_own);
@@ -807,6 +813,11 @@ static int ensure_scratch(pdeval_ctx* c, int64_t n) {
     if (c->d_ddps) (void)hipFree(c->d_ddps);
     c->d_ddps = nullptr;
     HIPCHK(c, hipMalloc(&c->d_ddps, cap));
+    if (c->d_dd_res) (void)hipFree(c->d_dd_res);
+    if (c->d_dd_q) (void)hipFree(c->d_dd_q);
+    c->d_dd_res = c->d_dd_q = nullptr;
+    HIPCHK(c, hipMalloc(&c->d_dd_res, cap * 4 * sizeof(double)));   // (n_ref <= 4)
+    HIPCHK(c, hipMalloc(&c->d_dd_q, cap * sizeof(double)));
     if (c->d_hseg) (void)hipFree(c->d_hseg);
     c->d_hseg = nullptr;
     if (c->hoist) {
@@ -987,6 +998,9 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     a.esc_count = cnt + L_ESC;
     a.pstate = c->d_pstate;
     a.ddps = c->d_ddps;
+    a.dd_res = c->d_dd_res;
+    a.dd_q = c->d_dd_q;
+    a.dd_spec = 0;   // (set in launch_all when the early tier runs)
     a.pdeep_list = c->d_list[L_PDEEP];
     a.pdeep_count = cnt + L_PDEEP;
     a.noise_ref = c->d_noise;
@@ -1041,6 +1055,10 @@ static int launch_all(pdeval_ctx* c, const int32_t* d_ops, int64_t n_words, cons
     // (below ~1,000 candidates the double-double tier is short and the fork only adds launches:
     // 512 candidates 2.40 vs 2.36 ms, 1,024: 2.89 vs 3.24 ms, profiles/r04_k_device_batch.log)
     const bool early = c->dd_early && n >= PD_DD_EARLY_MIN_N;
+    // the provisional point passes join the early tier speculatively (PD_DD_SPEC): the late tier
+    // after the grid -- on the critical path of every batch, 1.5 ms of a 4,096-candidate call,
+    // profiles/r06_g_device_batch.log -- is left with nothing but its collect pass
+    a.dd_spec = early && c->dd_spec ? 1 : 0;
     if (early) {
         // ---- the early double-double tier (pdeval_point.h): the candidates the point stage
         // left undecided or not accurate enough in fp64 are known now, so their evaluation runs

@@ -73,6 +73,13 @@ struct KernelArgs {
     int32_t* esc_count;
     uint8_t* pstate;            // point-stage state per candidate (P0_*), or NULL
     uint8_t* ddps;              // the early double-double tier's result per candidate (dd_point_kernel<DEFER>)
+    // (PD_DD_SPEC) the provisional point passes (P0_PROV) evaluated speculatively in the early
+    // tier: their res_ref / q_ref go to these side arrays (n * n_ref, n; a NaN sentinel where
+    // not written) and dd_apply_kernel copies them out only if the final class calls for the
+    // double-double value -- the rule the late tier applied after the grid
+    double* dd_res;
+    double* dd_q;
+    int dd_spec;
     int64_t* pdeep_list;        // real programs deeper than pass 0's stack: the deep point pass
     int32_t* pdeep_count;
     double* noise_ref;          // n * n_ref fp64 noise bounds at the reference points (point stage)

@@ -429,10 +429,12 @@ __global__ __launch_bounds__(256) void dd_collect_kernel(KernelArgs a) {
     if (cand < 0) return;
     const uint8_t ps = a.pstate[cand];
     if ((ps & 3) == P0_NONE) return;
+    // (a.dd_spec: the early tier also takes the provisional passes, speculatively)
+    const uint8_t early_bits = (uint8_t)(P0_DD | (a.dd_spec ? P0_PROV : 0));
     if (MODE == DD_EARLY) {
-        if (!(ps & P0_DD)) return;
+        if (!(ps & early_bits)) return;
     } else {
-        if (MODE == DD_LATE && (ps & P0_DD)) return;           // the early tier took it
+        if (MODE == DD_LATE && (ps & early_bits)) return;      // the early tier took it
         const uint8_t st = a.out.status[cand];
         const bool need = (MODE == DD_ALL && (ps & P0_DD)) ||
                           ((ps & P0_PROV) && (st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID ||
@@ -574,7 +576,7 @@ template <class T, int K, int MAXD, class V> struct ValInterp {
 // (P0_NONE: not evaluated -- program error or not finite, the fp64 decision stands).
 template <int PROB, class T, int MAXD, class STK>
 __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t cand, const int32_t* prog, int plen,
-                                                  uint32_t hdr, STK& stk) {
+                                                  uint32_t hdr, STK& stk, double* res_out, double* q_out) {
     constexpr int K = PROB == PDEVAL_PROBLEM_FORCE_FREE ? 4 : 2;
     constexpr int NC = nc(K);
     double qr = 0.0;
@@ -606,7 +608,7 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
 #pragma unroll
             for (int i = 0; i < NC; ++i) tiny = tiny && m[i] < kTinyJet;
             if (tiny) {   // underflowed: a passing point (kTinyJet)
-                if (a.out.res_ref) a.out.res_ref[cand * a.n_ref + p] = re_hi(res);
+                if (res_out) res_out[p] = re_hi(res);
                 qr = fmax(qr, res_abs);
                 continue;
             }
@@ -615,8 +617,7 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
 #pragma unroll
         for (int i = 0; i < NC; ++i) fin = fin && m[i] < kHugeJet;
         const double rr = re_hi(res), ri = im_hi(res);
-        if (isfinite(res_abs) && a.out.res_ref)
-            a.out.res_ref[cand * a.n_ref + p] = ri == 0.0 ? rr : copysign(res_abs, rr);
+        if (isfinite(res_abs) && res_out) res_out[p] = ri == 0.0 ? rr : copysign(res_abs, rr);
         if (!fin) {
             fin_all = false;
             continue;
@@ -635,7 +636,7 @@ __device__ __forceinline__ uint8_t dd_point_stage(const KernelArgs& a, int64_t c
     // a value beyond fp64): the reference's N(., 40) is zoo / nan / a float overflow there, a
     // reject either way (kerr validator.py:178-190).  Force-free keeps the fp64 decision.
     if (!fin_all) return PROB == PDEVAL_PROBLEM_FORCE_FREE ? P0_NONE : P0_REJECT;
-    if (a.out.q_ref) a.out.q_ref[cand] = qr;
+    if (q_out) *q_out = qr;
     if constexpr (PROB == PDEVAL_PROBLEM_FORCE_FREE) return ff & (3 | P0_NZ);
     else return rej ? P0_REJECT : (uint8_t)(nzk ? P0_PASS | P0_NZ : P0_PASS);
 }
@@ -667,6 +668,14 @@ __device__ __forceinline__ void dd_apply_one(const KernelArgs& a, int64_t cand, 
 
 // "keep the fp64 decision" in a.ddps (never a final class: those have no P0_DD bit)
 constexpr uint8_t kDdKeep = 0xfe;
+// a side-array value the double-double tier did not write (a quiet NaN it never produces: it
+// writes finite residuals only, and q_ref only when every point was finite)
+constexpr long long kDdUnset = 0x7ff8dead0000beefll;
+// an early-list entry that is a speculative provisional pass (not a P0_DD candidate)
+__device__ __forceinline__ bool dd_spec_entry(const KernelArgs& a, int64_t cand) {
+    const uint8_t ps = a.pstate[cand];
+    return a.dd_spec && (ps & P0_PROV) && !(ps & P0_DD);
+}
 
 // DEFER (the early lists, on the second stream while the grid passes run): the class goes to
 // a.ddps[cand] and dd_apply_kernel applies it after the grid; nothing else the grid passes
@@ -691,11 +700,21 @@ __global__ __launch_bounds__(64, MAXD == 2 ? PD_DD2_WAVES : 1) void dd_point_ker
         if (cand < 0) continue;
         int64_t beg, end;
         uint8_t s = P0_NONE;
+        double* res_out = a.out.res_ref ? a.out.res_ref + cand * a.n_ref : nullptr;
+        double* q_out = a.out.q_ref ? a.out.q_ref + cand : nullptr;
+        if (DEFER && dd_spec_entry(a, cand)) {
+            // a speculative provisional pass: its outputs to the side arrays, sentinel first
+            res_out = a.dd_res + cand * a.n_ref;
+            q_out = a.dd_q + cand;
+            for (int p = 0; p < a.n_ref; ++p) res_out[p] = __longlong_as_double(kDdUnset);
+            *q_out = __longlong_as_double(kDdUnset);
+        }
         if (prog_bounds(a, cand, &beg, &end)) {
             const int32_t* prog = a.ops + beg;
             const uint32_t hdr = (uint32_t)prog[0];
             // (the collect pass routes by depth)
-            if ((int)((hdr >> 8) & 0xffu) <= MAXD) s = dd_point_stage<PROB, T, MAXD>(a, cand, prog, (int)(end - beg), hdr, stk);
+            if ((int)((hdr >> 8) & 0xffu) <= MAXD)
+                s = dd_point_stage<PROB, T, MAXD>(a, cand, prog, (int)(end - beg), hdr, stk, res_out, q_out);
         }
         if constexpr (DEFER) {
             a.ddps[cand] = s == P0_NONE ? kDdKeep : s;
@@ -720,6 +739,18 @@ __global__ __launch_bounds__(256) void dd_apply_kernel(KernelArgs a) {
             a, wi < n0 ? a.defer_list[wi] : (wi < n0 + n1 ? a.cplx_list[wi - n0] : a.esc_list[wi - n0 - n1]), ERRW_DD_APPLY);
         if (cand < 0) continue;
         const uint8_t s = a.ddps[cand];
+        if (dd_spec_entry(a, cand)) {
+            // the late tier's rule: only where the final class may be overridden does the
+            // double-double value count (its outputs, then its class)
+            const uint8_t st = a.out.status ? a.out.status[cand] : (uint8_t)PDEVAL_CLS_ACCEPT;
+            if (!(st == PDEVAL_CLS_ACCEPT || st == PDEVAL_CLS_REJECT_GRID || st == PDEVAL_CLS_REJECT_SYMBOLIC)) continue;
+            if (a.out.res_ref)
+                for (int p = 0; p < a.n_ref; ++p) {
+                    const double v = a.dd_res[cand * a.n_ref + p];
+                    if (__double_as_longlong(v) != kDdUnset) a.out.res_ref[cand * a.n_ref + p] = v;
+                }
+            if (a.out.q_ref && __double_as_longlong(a.dd_q[cand]) != kDdUnset) a.out.q_ref[cand] = a.dd_q[cand];
+        }
         if (s != kDdKeep) dd_apply_one(a, cand, s);
     }
 }

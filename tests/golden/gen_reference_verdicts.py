@@ -19,6 +19,7 @@ Imports the reference from a scratch copy (see ``gen_streams.py``) and records, 
 """
 import argparse
 import gzip
+import queue as _queue
 import json
 import multiprocessing as mp
 import os
@@ -156,6 +157,72 @@ def _verdict_one(item):
     return rec
 
 
+def _hard_worker(init, tasks, results):
+    """A verdict worker of run_hard: announces each item before it starts it."""
+    _init_worker(*init)
+    while True:
+        item = tasks.get()
+        if item is None:
+            return
+        results.put(('start', os.getpid(), item, time.time()))
+        results.put(('done', os.getpid(), _verdict_one(item), 0.0))
+
+
+def run_hard(items, procs, init, hard_s, emit):
+    """The verdicts of ``items`` on ``procs`` forked workers, each item under a HARD deadline:
+    SIGALRM cannot interrupt SymPy inside a C-level call (one depth-5 row ran for an hour past its
+    20 s alarm), so the parent kills a worker whose item passed ``hard_s`` seconds, records the
+    item as undecided (timeout, ``hard_kill``) and starts a new worker for the rest.  ``emit``
+    receives every record as it completes."""
+    ctx = mp.get_context('fork')
+    tasks, results = ctx.Queue(), ctx.Queue()
+    for it in items:
+        tasks.put(it)
+    workers = {}
+
+    def spawn():
+        w = ctx.Process(target=_hard_worker, args=(init, tasks, results), daemon=True)
+        w.start()
+        workers[w.pid] = [w, None, 0.0]
+
+    for _ in range(procs):
+        spawn()
+    left = len(items)
+    while left:
+        try:
+            kind, pid, obj, t0 = results.get(timeout=2.0)
+            if kind == 'start':
+                workers[pid][1], workers[pid][2] = obj, t0
+            else:
+                workers[pid][1] = None
+                emit(obj)
+                left -= 1
+        except _queue.Empty:
+            pass
+        now = time.time()
+        for pid, (w, it, t0) in list(workers.items()):
+            if it is not None and now - t0 > hard_s:
+                w.kill()
+                w.join(5)
+                del workers[pid]
+                emit({'idx': it[0], 'depth': it[1], 'expr': it[2], 'ok': None, 'reason': None, 'timeout': True,
+                      't': round(now - t0, 1), 'hard_kill': True})
+                left -= 1
+                spawn()
+            elif not w.is_alive() and it is not None:   # died on its own (OOM, crash)
+                del workers[pid]
+                emit({'idx': it[0], 'depth': it[1], 'expr': it[2], 'ok': None, 'reason': 'worker died',
+                      'timeout': False, 't': round(now - t0, 1)})
+                left -= 1
+                spawn()
+    for _ in workers:
+        tasks.put(None)
+    for w, _, _ in workers.values():
+        w.join(10)
+        if w.is_alive():
+            w.kill()
+
+
 def read_stream(path):
     with gzip.open(path, 'rt') as f:
         return [(i, int(l.split('\t', 1)[0]), l.rstrip('\n').split('\t', 1)[1]) for i, l in enumerate(f)]
@@ -177,6 +244,8 @@ def main():
     ap.add_argument('--seed', type=int, default=0)
     ap.add_argument('--timeout', type=int, default=60)
     ap.add_argument('--procs', type=int, default=os.cpu_count())
+    ap.add_argument('--hard', type=int, default=0,
+                    help='per-item hard deadline in seconds (the parent kills a stuck worker); 0 = off')
     ap.add_argument('--kerr-a-value', default='1/10', help="Kerr validator's a_value")
     ap.add_argument('--ff-omega', default='0', help="force-free validator's Omega (a constant)")
     ap.add_argument('--kerr-op-a-zero', action='store_true',
@@ -229,6 +298,22 @@ def main():
     if a.sample and a.sample < len(items):
         items = sorted(random.Random(a.seed).sample(items, a.sample))
     init = (a.ref, a.problem, a.kerr_a_value, a.kerr_op_a_zero, a.ff_omega)
+    if a.hard:
+        with open(a.out, 'w') as f:
+            cnt = [0]
+
+            def emit(rec):
+                rec['problem'] = a.problem
+                if a.timeout != 60:
+                    rec['limit_s'] = a.timeout
+                f.write(json.dumps(rec) + '\n')
+                f.flush()
+                cnt[0] += 1
+                if cnt[0] % 50 == 0:
+                    print(f'[verdicts] {cnt[0]}/{len(items)} {time.time()-t0:.0f}s', flush=True)
+            run_hard(items, a.procs, init, a.hard, emit)
+        print(f'wrote {len(items)} verdicts to {a.out} in {time.time()-t0:.0f}s')
+        return
     with mp.get_context('fork').Pool(a.procs, _init_worker, init,
                                      maxtasksperchild=200) as pool, open(a.out, 'w') as f:
         n = 0

@@ -7,5 +7,5 @@ for start in $(seq ${FIRST:-0} 1000 10000); do
   out=ref/d5f_${start}_t20.jsonl
   [ -s "$out" ] && [ "$(wc -l < "$out")" -ge 1000 ] && continue
   python3 gen_reference_verdicts.py verdicts --input streams/force_free_d5_faithful.txt.gz \
-    --out "$out" --start "$start" --stop $((start + 1000)) --timeout 20 --procs "$PROCS" || exit 1
+    --out "$out" --start "$start" --stop $((start + 1000)) --timeout 20 --hard 90 --procs "$PROCS" || exit 1
 done

@@ -342,3 +342,34 @@ def test_dd_early_split_equals_single_tier(n):
     finally:
         e1.close()
         e0.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('problem, name, n', [('force_free', 'force_free_d4_validated', 0),
+                                              ('kerr_magnetosphere', 'kerr_magnetosphere_d4_stream', 200000)])
+def test_dd_speculative_provisional_equals_late(problem, name, n):
+    """PD_DD_SPEC: the provisional point passes (P0_PROV) run in the early double-double tier
+    beside the grid, their outputs held in side arrays and applied after the grid only where the
+    final class calls for them -- exactly the outputs of the late tier after the grid
+    (PDEVAL_DD_SPEC=0), on the whole force-free d4 workload and 200,000 Kerr d4 programs, at the
+    workload size and at a worker queue batch."""
+    from pdeval import problem_defs as P
+    from pdeval.workload import load_programs, gather_programs
+    pd_ = P.get(problem)
+    ops, off, _ = load_programs(name)
+    idx = np.arange(len(off) - 1)
+    if n:
+        idx = np.random.default_rng(0).choice(idx, n, replace=False)
+    on = _ctx_with_env(pd_.problem_id, {'PDEVAL_DD_SPEC': '1'})
+    no = _ctx_with_env(pd_.problem_id, {'PDEVAL_DD_SPEC': '0'})
+    try:
+        for sel in (idx, idx[:4096]):
+            o, f = gather_programs(ops, off, sel)
+            a, b = on.validate(o, f), no.validate(o, f)
+            for k in ('status', 'verdict', 'q_ref', 'res_ref', 'q_grid', 'n_bad', 'n_nonfinite', 'fingerprint'):
+                x = np.asarray(a[k])
+                assert np.array_equal(x, np.asarray(b[k]), equal_nan=x.dtype.kind == 'f'), (problem, len(sel), k)
+            assert on.device_error() == 0 and no.device_error() == 0
+    finally:
+        on.close()
+        no.close()
