@@ -143,6 +143,17 @@ FF_COUNT_SLACK = {
 # SymPy leaves the sqrt(rho/z) terms un-merged -- are reproduced by the 'replay' mode
 # (pdeval/symbolic.py); the default mode gives the true verdict.
 FF_D5 = ('ff_d5_s400.jsonl', 'ff_d5_s4000_t20.jsonl', 'ff_d5_s7000_t20.jsonl', 'ff_d5_s7600_t20.jsonl')
+# the faithful depth-5 sample (tests/golden/gen_d5_faithful.py: the reference's own enumerator
+# rules, normalize_batch, signature dedupe and pre-validate filters), the reference's verdicts at
+# the 20 s limit in 1,000-row chunks (tests/golden/run_d5f_verdicts.sh)
+def ff_d5f_files():
+    import glob
+    return tuple(sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, 'ref', 'd5f_*_t20.jsonl'))))
+
+
+# decided faithful-d5 rows where the default mode's verdict differs from the reference's (scored
+# by tests/golden/score_d5f.py with pdeval.symbolic.suspect frozen at commit 5708cbc): none
+FF_D5F_OFF_DIVERGENCE = frozenset()
 FF_D5_SYMBOLIC_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))'}
 # Every decided force-free fixture row on which the default mode ('off': the grid's det == 0
 # and the structural rules) and the reference's verdict differ -- all decided in the reference's

@@ -663,3 +663,25 @@ def test_plugin_range_rows_reference_verdicts():
     bad = [(r['expr'], r['ok'], g) for g, r in zip(got, rows) if g[0] != r['ok']]
     assert not bad, bad
     assert sum(g[0] for g in got) >= 10
+
+
+def test_plugin_api_depth5_faithful():
+    """configs[3]'s depth on the reference's OWN depth-5 distribution: the
+    faithful sample's decided rows (G.ff_d5f_files(); the suspect rule frozen before the sample
+    was drawn) through the plugin on the GPU, default mode: every verdict equals the
+    reference's except the rows G.FF_D5F_OFF_DIVERGENCE lists (none); reason texts are
+    reported."""
+    from problems import load_problem
+    import sympy as sp
+    files = G.ff_d5f_files()
+    if not files:
+        pytest.skip('no faithful d5 verdicts recorded')
+    rows = G.decided(G.ref_rows(*files))
+    prob = load_problem('force_free')
+    locs = {**prob.symbols, **prob.constants, **prob.unary_ops}
+    us = [sp.sympify(r['expr'], locals=locs) for r in rows]
+    got = prob.validator.validate_batch(us, check_regularity=False, fast_point_only=False)
+    wrong = {r['expr'] for g, r in zip(got, rows) if g[0] != r['ok']}
+    assert wrong <= G.FF_D5F_OFF_DIVERGENCE, sorted(wrong - G.FF_D5F_OFF_DIVERGENCE)[:20]
+    texts = sum(1 for g, r in zip(got, rows) if g[1] == r['reason'])
+    print(f'faithful d5: {len(rows)} decided rows, verdicts equal {len(rows) - len(wrong)}, texts equal {texts}')

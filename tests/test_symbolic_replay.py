@@ -219,3 +219,35 @@ def test_strict_stage_host_step():
     assert out['status'][1] == CLS_ACCEPT and 1 not in out['reason_override']
     assert out['status'][2] == CLS_ACCEPT and out['verdict'][2]
     assert out['strict'] == {'grid_zero': 3, 'suspect': 2, 'replayed': 2, 'timeouts': 0}
+
+
+def test_faithful_d5_sample_scores():
+    """The faithful depth-5 sample (tests/golden/gen_d5_faithful.py, the
+    reference's own enumerator rules and filters): on every decided row the default mode (the
+    device class -- the oracle's, held equal on the GPU -- through the host steps) and the
+    'strict' mode (pdeval.symbolic.suspect, frozen at commit 5708cbc before the sample was drawn;
+    the recorded replays of tests/golden/replay/d5f_replay.jsonl) give the reference's verdict
+    except the listed rows; the suspect rule's source is the frozen one."""
+    import hashlib
+    import inspect
+    import sys
+    sys.path.insert(0, os.path.join(G.GOLDEN))
+    import score_d5f
+    rs = score_d5f.rows()
+    if not rs:
+        pytest.skip('no faithful d5 verdicts recorded')
+    rp = os.path.join(G.GOLDEN, 'replay', 'd5f_replay.jsonl')
+    replays = {}
+    if os.path.exists(rp):
+        with open(rp) as f:
+            replays = {r['expr']: r for r in map(json.loads, f)}
+    summ, per = score_d5f.score(rs, replays)
+    # every suspect grid zero has its replay recorded (or the row keeps the device verdict)
+    missing = [p['expr'] for p in per if p['suspect'] and p['expr'] not in replays]
+    assert not missing, missing[:5]
+    assert set(summ['off_divergent']) <= G.FF_D5F_OFF_DIVERGENCE, summ['off_divergent'][:10]
+    assert not summ['strict_divergent'], summ['strict_divergent'][:10]
+    assert summ['decided'] >= 800, summ['decided']
+    with open(os.path.join(G.GOLDEN, 'ref', 'd5f_score.json')) as f:
+        frozen = json.load(f)['suspect_source_sha256']
+    assert hashlib.sha256(inspect.getsource(S.suspect).encode()).hexdigest() == frozen
