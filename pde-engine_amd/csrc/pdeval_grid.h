@@ -486,6 +486,12 @@ template <int W> struct PowTab {
 #ifndef PD_LEAN_PTR
 #define PD_LEAN_PTR 1
 #endif
+#ifndef PD_DISPATCH_FREQ
+#define PD_DISPATCH_FREQ 1
+#endif
+#ifndef PD_PIN_Y
+#define PD_PIN_Y 1
+#endif
 template <class T, int K, int W, int MAXD> struct Lean {
     using O = JetOps<T, K>;
     using J = typename O::J;
@@ -559,7 +565,7 @@ template <class T, int K, int W, int MAXD> struct Lean {
     // the pre-phase of a segment starts at its first opcode with the original word w0 and an
     // empty stack.
     template <bool XL = false, bool PRE = false>
-    static __device__ __forceinline__ void run(const int32_t* dec, const double (&x)[W], double y,
+    static __device__ __forceinline__ void run(const int32_t* dec, const double (&x)[W], double y_in,
                                                const double (&inv_x)[W], double inv_y, J (&acc)[W],
                                                T* stk, int lane, const PowTab<W>& pt, int pc0 = 1,
                                                int stop = 0, const double* h2 = nullptr, int h2row = 0,
@@ -581,6 +587,13 @@ template <class T, int K, int W, int MAXD> struct Lean {
         bool first = fresh || pc0 == 1;
         int d = first ? 0 : 1;   // operand stack depth (wave-uniform); MAXD = 2 needs only `first`
         for (;;) {
+            // (PD_PIN_Y) the lane's ordinate made opaque once per opcode: values derived from it
+            // (the powers y^k of a coordinate power) are formed where an opcode uses them instead
+            // of being hoisted out of the loop and kept live -- spilled to scratch -- through it
+            // (force-free only: same box, pass 1 129.4 -> 125.4 ms and its scratch frame 96 -> 64
+            // B/lane; Kerr's pass 1 went 48.5 -> 50.0 ms with it, profiles/r06_m_ab_*)
+            double y = y_in;
+            if constexpr (PD_PIN_Y && K == 4) pin_f64(y);
             const uint32_t op = w & 0xffu;
             const uint32_t grp = (w >> 17) & 7u;
             // group tests: a bit test on the one-hot copy (s_bitcmp + branch) or a compare of
@@ -619,33 +632,15 @@ template <class T, int K, int W, int MAXD> struct Lean {
                     }
                 }
                 ++d;
-                if (op == PDOP_PUSH_X) {
-#pragma unroll
-                    for (int q = 0; q < W; ++q) O::set_var(acc[q], x[q], 0);
-                } else if (op == PDOP_PUSH_P) {
-                    double pk[K + 1];
-                    if (on_y) {
-                        pco_y(pt, y, pn, pk);
-#pragma unroll
-                        for (int q = 0; q < W; ++q) O::template set_p<1>(acc[q], pk);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < W; ++q) {
-                            pco_x<XL>(pt, x, q, pn, pk);
-                            O::template set_p<0>(acc[q], pk);
-                        }
-                    }
-                } else if (op == PDOP_PUSH_Y) {
-#pragma unroll
-                    for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
-                } else if (PD_FUSE_PUSHC && K == 2 &&
-                           (op == PDOP_MUL_X || op == PDOP_MUL_Y || (PD_FUSE_PUSHC == 1 && op == PDOP_MUL_P))) {
-                    // a fused PUSH_C c + MUL_* (decode_kernel), in closed form: c (v + d_axis)
-                    // is (c v, c along the axis, 0 elsewhere) and c P = (c p_k along the axis).
-                    // These are the values set_const + mul_var / mul_p compute (their other
-                    // terms are products with exact zeros), without the products by zero
-                    // that the compiler may not fold (0 * v is -0 or NaN for some v) and kept
-                    // live across the loop -- which spilled 48 B per lane in round 3.
+                // a fused PUSH_C + MUL_X / MUL_Y / MUL_P of the decoder (Kerr), in closed form:
+                // c (v + d_axis) is (c v, c along the axis, 0 elsewhere) and c P = (c p_k along
+                // the axis) -- the values set_const + mul_var / mul_p compute (their other terms
+                // are products with exact zeros), without the products by zero that the compiler
+                // may not fold (0 * v is -0 or NaN for some v) and kept live across the loop,
+                // which spilled 48 B per lane in round 3
+                const bool fused = PD_FUSE_PUSHC && K == 2 &&
+                                   (op == PDOP_MUL_X || op == PDOP_MUL_Y || (PD_FUSE_PUSHC == 1 && op == PDOP_MUL_P));
+                auto fused_push = [&]() {
                     double pk[K + 1];
                     if (op == PDOP_MUL_P && on_y) pco_y(pt, y, pn, pk);
                     const T c = cvt<T>(cimm);
@@ -668,6 +663,32 @@ template <class T, int K, int W, int MAXD> struct Lean {
                             for (int k = 1; k <= K; ++k) acc[q].c[ji(k, 0)] = c * cvt<T>(pk[k]);
                         }
                     }
+                };
+                // (PD_DISPATCH_FREQ, Kerr: the fused push -- 1.5 of its 2.7 pushes per program --
+                // is tested first; the interpreter is scalar-issue bound there)
+                if (PD_DISPATCH_FREQ && K == 2 && fused) {
+                    fused_push();
+                } else if (op == PDOP_PUSH_X) {
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::set_var(acc[q], x[q], 0);
+                } else if (op == PDOP_PUSH_P) {
+                    double pk[K + 1];
+                    if (on_y) {
+                        pco_y(pt, y, pn, pk);
+#pragma unroll
+                        for (int q = 0; q < W; ++q) O::template set_p<1>(acc[q], pk);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < W; ++q) {
+                            pco_x<XL>(pt, x, q, pn, pk);
+                            O::template set_p<0>(acc[q], pk);
+                        }
+                    }
+                } else if (op == PDOP_PUSH_Y) {
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::set_var(acc[q], y, 1);
+                } else if (!PD_DISPATCH_FREQ && fused) {
+                    fused_push();
                 } else if (Real<T>::cplx_pass && op == PDOP_PUSH_I) {
                     if constexpr (Real<T>::cplx_pass) {
 #pragma unroll
@@ -692,6 +713,10 @@ template <class T, int K, int W, int MAXD> struct Lean {
                     const double c = cimm;
 #pragma unroll
                     for (int q = 0; q < W; ++q) acc[q].c[0] = acc[q].c[0] + cvt<T>(c);
+                } else if (PD_DISPATCH_FREQ && K == 2 && op == PDOP_MULC) {   // (1.2 per Kerr program; NEG is folded)
+                    const double c = cimm;
+#pragma unroll
+                    for (int q = 0; q < W; ++q) O::scale(acc[q], cvt<T>(c));
                 } else if (op == PDOP_NEG) {
 #pragma unroll
                     for (int q = 0; q < W; ++q) O::scale(acc[q], from_real<T>(-1.0));

@@ -24,6 +24,7 @@ import inspect
 import os
 import queue as _queue
 import sqlite3
+import sys
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -413,6 +414,13 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: Optional[in
         compilers = int(os.environ.get('PDEVAL_PIPE_COMPILERS', '4'))
     bv = validator._validator()
     sym = _symbolic_args(validator)
+    # the pipeline's threads hand the GIL to each other often: with the interpreter's default
+    # 5 ms switch interval, a thread back from a GIL-free C call (the device call, the native
+    # compile) can wait a whole interval for a stage thread holding it (PDEVAL_SWITCH_INTERVAL)
+    sw_old = sys.getswitchinterval()
+    sw = float(os.environ.get('PDEVAL_SWITCH_INTERVAL', '0.0005'))
+    if sw > 0:
+        sys.setswitchinterval(sw)
     strict = None
     if stream_strict and sym.get('symbolic') == 'strict' and bv.pd.slug == 'force_free':
         strict = StrictStream(bv, tagger, sym.get('symbolic_timeout') or bv.symbolic_timeout)
@@ -460,5 +468,6 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: Optional[in
             yield inflight.popleft().result()
             yield from resolved()
         yield from resolved(wait=True)
+    sys.setswitchinterval(sw_old)
     if strict is not None and stats is not None:
         stats.update(strict.stats)

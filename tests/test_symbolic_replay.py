@@ -227,7 +227,8 @@ def test_faithful_d5_sample_scores():
     device class -- the oracle's, held equal on the GPU -- through the host steps) and the
     'strict' mode (pdeval.symbolic.suspect, frozen at commit 5708cbc before the sample was drawn;
     the recorded replays of tests/golden/replay/d5f_replay.jsonl) give the reference's verdict
-    except the listed rows; the suspect rule's source is the frozen one."""
+    except the listed rows (G.FF_D5F_OFF_DIVERGENCE / G.FF_D5F_STRICT_DIVERGENCE: reference false
+    negatives on functions of rho/z); the suspect rule's source is the frozen one."""
     import hashlib
     import inspect
     import sys
@@ -246,7 +247,7 @@ def test_faithful_d5_sample_scores():
     missing = [p['expr'] for p in per if p['suspect'] and p['expr'] not in replays]
     assert not missing, missing[:5]
     assert set(summ['off_divergent']) <= G.FF_D5F_OFF_DIVERGENCE, summ['off_divergent'][:10]
-    assert not summ['strict_divergent'], summ['strict_divergent'][:10]
+    assert set(summ['strict_divergent']) <= G.FF_D5F_STRICT_DIVERGENCE, summ['strict_divergent'][:10]
     assert summ['decided'] >= 800, summ['decided']
     with open(os.path.join(G.GOLDEN, 'ref', 'd5f_score.json')) as f:
         frozen = json.load(f)['suspect_source_sha256']
