@@ -1624,9 +1624,9 @@ int pdeval_compile_batch_mt(int problem_id, const char* text, const int64_t* str
         !offsets || !status)
         return PDEVAL_ERR_ARG;
     if (n_threads <= 0) n_threads = (int)std::max(1u, std::thread::hardware_concurrency());
-    // chunks of 128 strings: a worker batch of 4,096 spreads over 16 threads (512 left half of
-    // them idle; the per-batch compile is on the worker pipeline's critical path)
-    const int64_t kChunk = 128;
+    // chunks of 512 strings (128 -- a 4,096-string batch over 16 threads instead of 8 -- made
+    // the worker pipeline slower: more threads against its own compile and stage threads)
+    const int64_t kChunk = 512;
     const int64_t n_chunks = (n + kChunk - 1) / kChunk;
     if (n_threads > n_chunks) n_threads = (int)std::max<int64_t>(1, n_chunks);
     if (n_threads <= 1) return pdeval_compile_batch(problem_id, text, str_offsets, n, ops, ops_cap, offsets,

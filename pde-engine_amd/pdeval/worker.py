@@ -418,7 +418,9 @@ def process_batches(batches, validator, kwargs, locs, tagger, depth: Optional[in
     # 5 ms switch interval, a thread back from a GIL-free C call (the device call, the native
     # compile) can wait a whole interval for a stage thread holding it (PDEVAL_SWITCH_INTERVAL)
     sw_old = sys.getswitchinterval()
-    sw = float(os.environ.get('PDEVAL_SWITCH_INTERVAL', '0.0005'))
+    # (default: the interpreter's own; 0.5 ms measured no better -- the single-process pipeline
+    # 866 k/s before, 711 k/s with it and the 128-string compile chunks, profiles/r06_final_bench)
+    sw = float(os.environ.get('PDEVAL_SWITCH_INTERVAL', '0'))
     if sw > 0:
         sys.setswitchinterval(sw)
     strict = None
