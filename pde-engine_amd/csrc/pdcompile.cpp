@@ -34,6 +34,7 @@
 #include <deque>
 #include <string>
 #include <thread>
+#include <memory>
 #include <unordered_map>
 #include <vector>
 
@@ -140,6 +141,50 @@ std::string rstr(Rat a) {
     return s;
 }
 
+// per-thread bump arena for the evaluator's temporary vectors (TVec): compile_one rewinds it
+// at the start of every string, when no temporary of the previous string is alive; freeing the
+// most recent allocation rolls the bump pointer back (a growing vector reuses its own block)
+struct Arena {
+    static constexpr size_t kBlock = 1 << 20;
+    std::vector<std::unique_ptr<char[]>> blocks;
+    std::vector<size_t> sizes;
+    size_t bi = 0, off = 0;
+    void* get(size_t n, size_t al) {
+        for (;;) {
+            if (bi < blocks.size()) {
+                const size_t o = (off + al - 1) & ~(al - 1);
+                if (o + n <= sizes[bi]) {
+                    off = o + n;
+                    return blocks[bi].get() + o;
+                }
+                ++bi;
+                off = 0;
+                continue;
+            }
+            const size_t sz = n + al > kBlock ? n + al : kBlock;
+            blocks.emplace_back(new char[sz]);
+            sizes.push_back(sz);
+        }
+    }
+    void put(void* p, size_t n) {
+        if (bi < blocks.size() && (char*)p + n == blocks[bi].get() + off) off -= n;
+    }
+    void rewind() { bi = 0; off = 0; }
+};
+thread_local Arena g_arena;
+
+template <class T>
+struct ArenaAlloc {
+    using value_type = T;
+    ArenaAlloc() noexcept {}
+    template <class U> ArenaAlloc(const ArenaAlloc<U>&) noexcept {}
+    T* allocate(size_t n) { return (T*)g_arena.get(n * sizeof(T), alignof(T)); }
+    void deallocate(T* p, size_t n) noexcept { g_arena.put(p, n * sizeof(T)); }
+    template <class U> bool operator==(const ArenaAlloc<U>&) const noexcept { return true; }
+    template <class U> bool operator!=(const ArenaAlloc<U>&) const noexcept { return false; }
+};
+template <class T> using TVec = std::vector<T, ArenaAlloc<T>>;
+
 // ------------------------------------------------------------------ the expression DAG
 enum Kind : uint8_t { NUM, SYM, ADD, MUL, POW, EXP, ABS, IMAG };   // IMAG: SymPy's I
 
@@ -166,64 +211,177 @@ const SymInfo kKerrSyms[] = {{"r", 0, true, -1}, {"x", 1, false, -1},
 // three-valued logic for SymPy's assumption queries
 enum Tri : int8_t { NO = 0, YES = 1, UNK = 2 };
 
+// node storage in fixed chunks: references stay valid while evaluation appends new nodes, and
+// a reset keeps the chunks, so a reused slot's key string and argument vector keep their heap
+// capacity (one compile_one per string resets the table; most strings then allocate nothing)
+struct NodeStore {
+    static constexpr int kShift = 10;
+    std::vector<std::unique_ptr<Node[]>> chunks;
+    size_t n = 0;
+    Node& operator[](size_t i) { return chunks[i >> kShift][i & ((1u << kShift) - 1)]; }
+    const Node& operator[](size_t i) const { return chunks[i >> kShift][i & ((1u << kShift) - 1)]; }
+    size_t size() const { return n; }
+    void clear() { n = 0; }
+    Node& alloc() {
+        if ((n >> kShift) >= chunks.size()) chunks.emplace_back(new Node[1u << kShift]);
+        return (*this)[n++];
+    }
+};
+
 struct Ctx {
     const SymInfo* syms = nullptr;
     int nsyms = 0;
-    // a deque: references to nodes stay valid while evaluation appends new ones
-    std::deque<Node> nodes;
-    std::unordered_map<std::string, int> intern;
+    NodeStore nodes;
+    // hash consing on a STRUCTURAL key: the node kind and its children's ids (their canonical
+    // strings are interned, so the ids stand for them one to one), a rational's (p, q), a
+    // symbol's index.  Equal structural keys <=> equal canonical strings, so the nodes and their
+    // order are those of a string-keyed table; the canonical string of a node is built only
+    // when the node is new (it orders ADD/MUL arguments and is the pdeval_canonical output).
+    // Open addressing (linear probing) over node ids; a generation stamp clears it in O(1).
+    std::vector<int32_t> slot_id;
+    std::vector<uint32_t> slot_gen;
+    std::vector<uint64_t> slot_hash;
+    uint32_t gen = 0;
+    size_t used = 0;
     int ZERO = -1, ONE = -1, NEG1 = -1, IU = -1;
 
+    static uint64_t mix(uint64_t h, uint64_t v) {
+        h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+        return h * 0xff51afd7ed558ccdull;
+    }
+    void table_init(size_t cap) {
+        slot_id.assign(cap, -1);
+        slot_gen.assign(cap, 0);
+        slot_hash.assign(cap, 0);
+        gen = 1;
+        used = 0;
+    }
     void reset(const SymInfo* s, int n) {
         syms = s;
         nsyms = n;
         nodes.clear();
-        intern.clear();
+        if (slot_id.empty()) table_init(1 << 12);
+        if (++gen == 0) table_init(slot_id.size());
+        used = 0;
         ZERO = num(Rat{0, 1});
         ONE = num(Rat{1, 1});
         NEG1 = num(Rat{-1, 1});
-        IU = make(Node{IMAG, {}, -1, {}, "I"});
+        const uint64_t h = mix((uint64_t)IMAG, 0);
+        size_t pos = 0;
+        IU = lookup(h, IMAG, nullptr, 0, Rat{}, -1, &pos);
+        if (IU < 0) {
+            Node& nd = fresh(h, pos);
+            nd.k = IMAG;
+            nd.key = "I";
+            IU = (int)nodes.size() - 1;
+        }
     }
     const Node& N(int i) const { return nodes[i]; }
-    int make(Node&& nd) {
-        auto it = intern.find(nd.key);
-        if (it != intern.end()) return it->second;
+    bool same(const Node& nd, Kind k, const int* a, size_t na, Rat r, int sym) const {
+        if (nd.k != k) return false;
+        if (k == NUM) return nd.r.p == r.p && nd.r.q == r.q;
+        if (k == SYM) return nd.sym == sym;
+        if (nd.a.size() != na) return false;
+        for (size_t j = 0; j < na; ++j)
+            if (nd.a[j] != a[j]) return false;
+        return true;
+    }
+    // the node with this structural key, or -1 with *pos the free slot it would take
+    int lookup(uint64_t h, Kind k, const int* a, size_t na, Rat r, int sym, size_t* pos) const {
+        const size_t mask = slot_id.size() - 1;
+        for (size_t i = h & mask;; i = (i + 1) & mask) {
+            if (slot_gen[i] != gen) { *pos = i; return -1; }
+            if (slot_hash[i] == h && same(nodes[slot_id[i]], k, a, na, r, sym)) return slot_id[i];
+        }
+    }
+    // a new node slot (its fields still hold an earlier string's node: the caller sets them all)
+    Node& fresh(uint64_t h, size_t pos) {
         if (nodes.size() > 200000) throw Decline{};
         const int id = (int)nodes.size();
-        intern.emplace(nd.key, id);
-        nodes.push_back(std::move(nd));
-        return id;
+        slot_id[pos] = id;
+        slot_gen[pos] = gen;
+        slot_hash[pos] = h;
+        if (2 * ++used > slot_id.size()) grow();
+        Node& nd = nodes.alloc();
+        nd.r = Rat{};
+        nd.sym = -1;
+        nd.a.clear();
+        return nd;
+    }
+    void grow() {
+        std::vector<int32_t> id2(slot_id.size() * 2, -1);
+        std::vector<uint32_t> g2(id2.size(), 0);
+        std::vector<uint64_t> h2(id2.size(), 0);
+        const size_t mask = id2.size() - 1;
+        for (size_t i = 0; i < slot_id.size(); ++i) {
+            if (slot_gen[i] != gen) continue;
+            size_t j = slot_hash[i] & mask;
+            while (g2[j] == gen) j = (j + 1) & mask;
+            id2[j] = slot_id[i];
+            g2[j] = gen;
+            h2[j] = slot_hash[i];
+        }
+        slot_id.swap(id2);
+        slot_gen.swap(g2);
+        slot_hash.swap(h2);
     }
     int num(Rat r) {
-        Node nd{NUM, r, -1, {}, rstr(r)};
-        return make(std::move(nd));
+        const uint64_t h = mix(mix(mix((uint64_t)NUM, 0), (uint64_t)r.p), (uint64_t)r.q);
+        size_t pos = 0;
+        const int hit = lookup(h, NUM, nullptr, 0, r, -1, &pos);
+        if (hit >= 0) return hit;
+        Node& nd = fresh(h, pos);
+        nd.k = NUM;
+        nd.r = r;
+        nd.key = rstr(r);
+        return (int)nodes.size() - 1;
     }
     int sym(int s) {
-        Node nd{SYM, {}, s, {}, syms[s].name};
-        return make(std::move(nd));
+        const uint64_t h = mix(mix((uint64_t)SYM, 0), (uint64_t)s);
+        size_t pos = 0;
+        const int hit = lookup(h, SYM, nullptr, 0, Rat{}, s, &pos);
+        if (hit >= 0) return hit;
+        Node& nd = fresh(h, pos);
+        nd.k = SYM;
+        nd.sym = s;
+        nd.key = syms[s].name;
+        return (int)nodes.size() - 1;
+    }
+    uint64_t hash_args(Kind k, const int* a, size_t na) const {
+        uint64_t h = mix((uint64_t)k, na);
+        for (size_t j = 0; j < na; ++j) h = mix(h, (uint64_t)(uint32_t)a[j]);
+        return h;
+    }
+    // a node with children: found, or made with key = pre + child keys joined by ',' + ')'
+    int make_args(Kind k, const int* a, size_t na, const char* pre) {
+        const uint64_t h = hash_args(k, a, na);
+        size_t pos = 0;
+        const int hit = lookup(h, k, a, na, Rat{}, -1, &pos);
+        if (hit >= 0) return hit;
+        Node& nd = fresh(h, pos);
+        nd.k = k;
+        nd.a.assign(a, a + na);
+        nd.key = pre;
+        for (size_t i = 0; i < na; ++i) {
+            if (i) nd.key += ',';
+            nd.key += nodes[a[i]].key;
+        }
+        nd.key += ')';
+        return (int)nodes.size() - 1;
     }
     // raw constructors (no evaluation): children are already canonical
-    int raw_nary(Kind k, std::vector<int> args) {
+    int raw_nary(Kind k, TVec<int> args) {
         if (args.size() == 1) return args[0];
-        std::sort(args.begin(), args.end(), [&](int x, int y) { return nodes[x].key < nodes[y].key; });
-        std::string key = k == ADD ? "A(" : "M(";
-        for (size_t i = 0; i < args.size(); ++i) {
-            if (i) key += ",";
-            key += nodes[args[i]].key;
-        }
-        key += ")";
-        Node nd{k, {}, -1, std::move(args), std::move(key)};
-        return make(std::move(nd));
+        std::sort(args.begin(), args.end(),
+                  [&](int x, int y) { return x != y && nodes[x].key < nodes[y].key; });
+        return make_args(k, args.data(), args.size(), k == ADD ? "A(" : "M(");
     }
     int raw_pow(int b, int e) {
-        std::string key = "P(" + nodes[b].key + "," + nodes[e].key + ")";
-        Node nd{POW, {}, -1, {b, e}, std::move(key)};
-        return make(std::move(nd));
+        const int a[2] = {b, e};
+        return make_args(POW, a, 2, "P(");
     }
     int raw_fn(Kind k, int a) {
-        std::string key = std::string(k == EXP ? "E(" : "B(") + nodes[a].key + ")";
-        Node nd{k, {}, -1, {a}, std::move(key)};
-        return make(std::move(nd));
+        return make_args(k, &a, 1, k == EXP ? "E(" : "B(");
     }
     bool is_num(int i) const { return nodes[i].k == NUM; }
     Rat rv(int i) const { return nodes[i].r; }
@@ -343,7 +501,7 @@ struct Ctx {
             // args are sorted by key, so the (single) numeric coefficient may sit anywhere
             for (size_t j = 0; j < n.a.size(); ++j)
                 if (is_num(n.a[j])) {
-                    std::vector<int> rest;
+                    TVec<int> rest;
                     for (size_t k = 0; k < n.a.size(); ++k)
                         if (k != j) rest.push_back(n.a[k]);
                     return {rv(n.a[j]), raw_nary(MUL, rest)};
@@ -359,7 +517,7 @@ struct Ctx {
         const Rat cc = rmul(c, cm.first);
         if (req(cc, Rat{1, 1})) return cm.second;
         if (cc.p == 0) return ZERO;
-        std::vector<int> args{num(cc)};
+        TVec<int> args{num(cc)};
         if (nodes[cm.second].k == MUL) {
             for (int x : nodes[cm.second].a) args.push_back(x);
         } else if (cm.second != ONE) {
@@ -369,11 +527,11 @@ struct Ctx {
     }
 
     // ---------------------------------------------------------------- Add (Add.flatten)
-    int add(const std::vector<int>& in) {
+    int add(const TVec<int>& in) {
         Rat coeff{0, 1};
-        std::vector<int> order;
+        TVec<int> order;
         std::unordered_map<int, Rat> terms;
-        std::vector<int> seq(in.begin(), in.end());
+        TVec<int> seq(in.begin(), in.end());
         for (size_t i = 0; i < seq.size(); ++i) {
             const int o = seq[i];
             const Node& n = nodes[o];
@@ -384,13 +542,13 @@ struct Ctx {
             if (it == terms.end()) { terms.emplace(cm.second, cm.first); order.push_back(cm.second); }
             else it->second = radd(it->second, cm.first);
         }
-        std::vector<int> out;
+        TVec<int> out;
         for (int s : order) {
             const Rat c = terms[s];
             if (c.p == 0) continue;
             if (req(c, Rat{1, 1})) { out.push_back(s); continue; }
             if (nodes[s].k == MUL) {
-                std::vector<int> args{num(c)};
+                TVec<int> args{num(c)};
                 for (int x : nodes[s].a) args.push_back(x);
                 out.push_back(raw_nary(MUL, args));
             } else {
@@ -406,7 +564,7 @@ struct Ctx {
     struct BE { int base; Rat c; int term; };   // base ** (c * term); base -1 = E (exp)
     // Mul(*in, *[Pow(b, e, evaluate=False) for (b, e) in pre]): `pre` are unevaluated powers,
     // which Mul.flatten collects by their own base and re-evaluates in its rebuild
-    int mul(std::vector<int> in, const std::vector<BE>& pre = {}) {
+    int mul(TVec<int> in, const TVec<BE>& pre = {}) {
         in.erase(std::remove(in.begin(), in.end(), ONE), in.end());
         if (pre.empty() && in.empty()) return ONE;
         if (pre.empty() && in.size() == 1) return in[0];
@@ -415,14 +573,14 @@ struct Ctx {
             if (is_num(b) && !is_num(a)) std::swap(a, b);
             if (is_num(a) && rv(a).p != 0 && nodes[b].k == ADD) {
                 // 2-arg Rational * Add distributes (Mul.flatten's 2-arg hack)
-                std::vector<int> ts;
+                TVec<int> ts;
                 for (int t : nodes[b].a) ts.push_back(keep_coeff(rv(a), t));
                 return add(ts);
             }
         }
         Rat coeff{1, 1};
-        std::vector<BE> pw;
-        std::vector<int> seq(in.begin(), in.end());
+        TVec<BE> pw;
+        TVec<int> seq(in.begin(), in.end());
         for (const BE& x : pre) {
             if (is_num(x.base)) {   // Pow(Number, Integer) folds into the coefficient
                 if (rint(x.c)) coeff = rmul(coeff, rpow_int(rv(x.base), x.c.p));
@@ -433,7 +591,7 @@ struct Ctx {
         }
         // numeric bases with rational powers (pnum_rat), base -> exponents, insertion order;
         // neg1e, the exponent of -1 collected from I and from negative numeric bases
-        std::vector<std::pair<Rat, std::vector<Rat>>> pnum_rat;
+        TVec<std::pair<Rat, TVec<Rat>>> pnum_rat;
         Rat neg1e{0, 1};
         for (size_t i = 0; i < seq.size(); ++i) {
             const int o = seq[i];
@@ -467,10 +625,10 @@ struct Ctx {
             pw.push_back(BE{o, Rat{1, 1}, ONE});
         }
         if (coeff.p == 0) return ZERO;
-        std::vector<int> part;
+        TVec<int> part;
         for (int iter = 0; iter < 2; ++iter) {
             // _gather: combine the coefficients of equal (base, term)
-            std::vector<BE> g;
+            TVec<BE> g;
             for (const BE& x : pw) {
                 bool found = false;
                 for (BE& y : g)
@@ -478,7 +636,7 @@ struct Ctx {
                 if (!found) g.push_back(x);
             }
             part.clear();
-            std::vector<BE> np;
+            TVec<BE> np;
             bool changed = false;
             for (const BE& x : g) {
                 if (x.c.p == 0) continue;
@@ -509,7 +667,7 @@ struct Ctx {
             break;
         }
         // the rebuilt powers may be numbers or products (Pow of a Mul base): fold them in
-        std::vector<int> fac;
+        TVec<int> fac;
         for (int p : part) {
             const Node& n = nodes[p];
             if (n.k == NUM) coeff = rmul(coeff, n.r);
@@ -528,7 +686,7 @@ struct Ctx {
         if (coeff.p == 0) return ZERO;
         if (fac.empty()) return num(coeff);
         if (fac.size() == 1 && nodes[fac[0]].k == ADD && !req(coeff, Rat{1, 1})) {
-            std::vector<int> ts;
+            TVec<int> ts;
             for (int t : nodes[fac[0]].a) ts.push_back(mul({num(coeff), t}));
             return add(ts);
         }
@@ -550,7 +708,7 @@ struct Ctx {
         if (n.k == NUM) return num(rneg(n.r));
         if (n.k == ADD) return mul({NEG1, a});
         if (n.k == MUL) {
-            std::vector<int> args;
+            TVec<int> args;
             bool had = false;
             for (int c : n.a) {
                 if (!had && is_num(c)) {
@@ -592,7 +750,7 @@ struct Ctx {
             // factor-wise (only when every factor is decided without an Abs; SymPy keeps the
             // undecided ones under one unevaluated Abs)
             if (has_nested_add(a)) throw Decline{};   // signsimp would rewrite them first
-            std::vector<int> known;
+            TVec<int> known;
             for (int c : n.a) {
                 const Node& cn = nodes[c];
                 if (cn.k == POW && is_num(cn.a[1]) && rint(rv(cn.a[1])) && rv(cn.a[1]).p < 0) {
@@ -773,13 +931,13 @@ struct Ctx {
         // a perfect root: sqrt(4) -> 2
         const int64_t x = nthroot_exact(b, e.q);
         if (x >= 0) return num(Rat{ipow_checked(x, e.p), 1});
-        std::vector<std::pair<int64_t, int64_t>> dict;
+        TVec<std::pair<int64_t, int64_t>> dict;
         int64_t pb, pe;
         if (perfect_power(b, &pb, &pe)) dict.push_back({pb, pe});
-        else dict = factorint(b);
+        else { const auto f = factorint(b); dict.assign(f.begin(), f.end()); }
         int64_t out_int = 1, sqr_gcd = 0;
         int out_rad = -1;   // product of the extracted radicals (None: 1)
-        std::vector<std::pair<int64_t, int64_t>> sqr;
+        TVec<std::pair<int64_t, int64_t>> sqr;
         for (const auto& pr : dict) {
             const int64_t ex = pr.second * e.p;
             const int64_t de = ex / e.q, dm = ex % e.q;
@@ -811,10 +969,10 @@ struct Ctx {
 
     // Mul.flatten's numeric powers (part 2 of sympy/core/mul.py): pnum_rat, base -> exponents
     // in insertion order; returns the factors to add to the product, folds numbers into coeff
-    void numeric_powers(const std::vector<std::pair<Rat, std::vector<Rat>>>& pnum_rat, Rat& coeff,
-                        std::vector<int>& fac) {
+    void numeric_powers(const TVec<std::pair<Rat, TVec<Rat>>>& pnum_rat, Rat& coeff,
+                        TVec<int>& fac) {
         // comb_e: summed exponent -> bases
-        std::vector<std::pair<Rat, std::vector<Rat>>> comb;
+        TVec<std::pair<Rat, TVec<Rat>>> comb;
         for (const auto& be : pnum_rat) {
             Rat es{0, 1};
             for (Rat r : be.second) es = radd(es, r);
@@ -823,7 +981,7 @@ struct Ctx {
                 if (req(c.first, es)) { c.second.push_back(be.first); found = true; break; }
             if (!found) comb.push_back({es, {be.first}});
         }
-        std::vector<std::pair<Rat, Rat>> num_rat;   // (base, exponent)
+        TVec<std::pair<Rat, Rat>> num_rat;   // (base, exponent)
         for (auto& c : comb) {
             Rat bb{1, 1};
             for (Rat r : c.second) bb = rmul(bb, r);
@@ -836,7 +994,7 @@ struct Ctx {
             num_rat.push_back({bb, e});
         }
         // gcd extraction: 2**(1/3)*6**(1/4) -> 2**(1/3+1/4) * 3**(1/4)
-        std::vector<std::pair<Rat, std::vector<Rat>>> pnew;   // exponent -> bases
+        TVec<std::pair<Rat, TVec<Rat>>> pnew;   // exponent -> bases
         auto rgcd = [](Rat a, Rat b) {   // Rational.gcd: gcd of numerators / lcm of denominators
             const int64_t g = igcd(a.p, b.p), l = a.q / igcd(a.q, b.q) * b.q;
             return mkrat(g, l);
@@ -845,7 +1003,7 @@ struct Ctx {
             Rat bi = num_rat[i].first;
             const Rat ei = num_rat[i].second;
             if (req(bi, Rat{1, 1})) continue;
-            std::vector<std::pair<Rat, Rat>> grow;
+            TVec<std::pair<Rat, Rat>> grow;
             for (size_t j = i + 1; j < num_rat.size(); ++j) {
                 const Rat bj = num_rat[j].first, ej = num_rat[j].second;
                 const Rat g = rgcd(bi, bj);
@@ -867,8 +1025,8 @@ struct Ctx {
             }
             if (!req(bi, Rat{1, 1})) {
                 const int obj = pow_(num(bi), num(ei));
-                std::vector<int> parts;
-                if (nodes[obj].k == MUL) parts = nodes[obj].a;
+                TVec<int> parts;
+                if (nodes[obj].k == MUL) parts.assign(nodes[obj].a.begin(), nodes[obj].a.end());
                 else parts.push_back(obj);
                 for (int f : parts) {
                     const Node& fn = nodes[f];
@@ -896,16 +1054,16 @@ struct Ctx {
     // Mul._eval_power + Pow._eval_expand_power_base(force=False)
     int pow_mul(int b, int e) {
         const Rat ex = rv(e);
-        const std::vector<int> args = nodes[b].a;
+        const TVec<int> args(nodes[b].a.begin(), nodes[b].a.end());
         if (rint(ex)) {
             // Mul(*[Pow(f, e, evaluate=False) for f in args])
-            std::vector<BE> pre;
+            TVec<BE> pre;
             for (int c : args) pre.push_back(BE{c, ex, ONE});
             // ... * Pow(Mul._from_args(nc), e, evaluate=False): a second flatten, which
             // merges the products the first one produced
             return mul({mul({}, pre)}, {BE{ONE, ex, ONE}});
         }
-        std::vector<int> nonneg_, negs, other;
+        TVec<int> nonneg_, negs, other;
         for (int c : args) {
             const Tri t = nonneg(c);
             if (t == YES) nonneg_.push_back(c);
@@ -930,20 +1088,20 @@ struct Ctx {
         // for b in npow]); then rv *= Mul(*[Pow(c, e, evaluate=False) for c in the rest]) and
         // rv *= Pow(Mul(*other), e, evaluate=False)
         {
-            std::vector<int> npow, rest;
+            TVec<int> npow, rest;
             for (int c : nonneg_) {
                 const Node& cn = nodes[c];
                 if (cn.k == POW && is_num(cn.a[0]) && is_num(cn.a[1])) npow.push_back(c);
                 else rest.push_back(c);
             }
             if (!npow.empty()) {
-                std::vector<int> ps;
+                TVec<int> ps;
                 for (int c : npow) ps.push_back(pow_(c, e));
                 int rv = ps.size() == 1 ? ps[0] : mul(ps);
                 if (rest.size() == 1) {
                     rv = mul({rv}, {BE{rest[0], ex, ONE}});
                 } else if (!rest.empty()) {
-                    std::vector<BE> pr;
+                    TVec<BE> pr;
                     for (int c : rest) pr.push_back(BE{c, ex, ONE});
                     rv = mul({rv, mul({}, pr)});
                 }
@@ -956,7 +1114,7 @@ struct Ctx {
         }
         // rv = Mul(*[Pow(c, e, evaluate=False) for c in nonneg]); rv *= Pow(Mul(*other), e,
         // evaluate=False)  (a one-factor Mul of an unevaluated Pow is that Pow itself)
-        std::vector<BE> pre;
+        TVec<BE> pre;
         for (int c : nonneg_) pre.push_back(BE{c, ex, ONE});
         if (other.empty()) return pre.size() == 1 ? pow_(pre[0].base, e) : mul({}, pre);
         const int ob = other.size() == 1 ? other[0] : mul(other);
@@ -1097,7 +1255,7 @@ struct IR {
 
 struct Lower {
     Ctx& C;
-    std::vector<IR> ir;
+    TVec<IR> ir;
     explicit Lower(Ctx& c) : C(c) {}
     int mk(IR x) { ir.push_back(x); return (int)ir.size() - 1; }
     static double rdouble(Rat r) { return (double)r.p / (double)r.q; }   // exact p, q: correctly rounded
@@ -1167,14 +1325,14 @@ struct Lower {
         throw Decline{};
     }
     // stable sort by key, like Python's list.sort
-    template <class T, class K> static void ssort(std::vector<T>& v, K key) {
+    template <class T, class K> static void ssort(TVec<T>& v, K key) {
         std::stable_sort(v.begin(), v.end(), [&](const T& x, const T& y) { return key(x) < key(y); });
     }
     int add(int e) {
         const Node& nd = C.N(e);
         Rat cs{0, 1};
         bool have = false;
-        std::vector<std::pair<int, int>> terms;   // (sign, ir)
+        TVec<std::pair<int, int>> terms;   // (sign, ir)
         for (int t : nd.a) {
             if (C.is_num(t)) { cs = radd(cs, C.rv(t)); have = true; continue; }
             int sg = 1;
@@ -1206,8 +1364,8 @@ struct Lower {
     int mulnode(int e) { return mulargs(e, Rat{1, 1}); }
     // flatten.py _Lower.mul over the factors of e (a Mul or a single factor) times coefficient
     int mulargs(int e, Rat extra) {
-        std::vector<int> fs;
-        if (C.N(e).k == MUL) fs = C.N(e).a;
+        TVec<int> fs;
+        if (C.N(e).k == MUL) fs.assign(C.N(e).a.begin(), C.N(e).a.end());
         else if (e != C.ONE) fs.push_back(e);
         Rat coef{1, 1};
         bool first = true;
@@ -1216,7 +1374,7 @@ struct Lower {
             first = false;
         };
         if (!req(extra, Rat{1, 1})) mulc(extra);
-        std::vector<int> num, den;
+        TVec<int> num, den;
         for (int f : fs) {
             const Node& fn = C.N(f);
             if (fn.k == NUM) { mulc(fn.r); continue; }
@@ -1231,7 +1389,7 @@ struct Lower {
         (void)first;
         ssort(num, [&](int x) { return -need(x); });
         ssort(den, [&](int x) { return -need(x); });
-        auto product = [&](const std::vector<int>& v) {
+        auto product = [&](const TVec<int>& v) {
             int acc = v[0];
             for (size_t k = 1; k < v.size(); ++k) acc = bin(IMUL, acc, v[k]);
             return acc;
@@ -1267,11 +1425,11 @@ struct Lower {
     // ---- det_rational (flatten.py _det_kind / det_rational)
     struct Kd {
         int t;                    // 0 = None, 1 = 'R', 2 = 'C', 3 = ('P', exps, pure, sig), 4 = 'I'
-        std::vector<Rat> ex;
+        TVec<Rat> ex;
         bool pure = false;
         // sig: prod h**a, exponents summed per base (flatten.py _sig); bases are IR subtrees
         // compared structurally (the IR is not hash-consed)
-        std::vector<std::pair<int, Rat>> sig;
+        TVec<std::pair<int, Rat>> sig;
     };
     bool same(int i, int j) const {
         if (i == j) return true;
@@ -1282,21 +1440,21 @@ struct Lower {
             return false;
         return same(x.a, y.a) && same(x.b, y.b);
     }
-    std::vector<std::pair<int, Rat>> mksig(const std::vector<std::pair<int, Rat>>& pairs) const {
-        std::vector<std::pair<int, Rat>> acc;
+    TVec<std::pair<int, Rat>> mksig(const TVec<std::pair<int, Rat>>& pairs) const {
+        TVec<std::pair<int, Rat>> acc;
         for (const auto& pr : pairs) {
             bool found = false;
             for (auto& q : acc)
                 if (same(q.first, pr.first)) { q.second = radd(q.second, pr.second); found = true; break; }
             if (!found) acc.push_back(pr);
         }
-        std::vector<std::pair<int, Rat>> out;
+        TVec<std::pair<int, Rat>> out;
         for (const auto& q : acc) if (q.second.p != 0) out.push_back(q);
         return out;
     }
     // the irrational part: exponents modulo 1, integer powers dropped (flatten.py _irr)
-    std::vector<std::pair<int, Rat>> irr(const std::vector<std::pair<int, Rat>>& sg) const {
-        std::vector<std::pair<int, Rat>> out;
+    TVec<std::pair<int, Rat>> irr(const TVec<std::pair<int, Rat>>& sg) const {
+        TVec<std::pair<int, Rat>> out;
         for (const auto& q : sg) {
             Rat f = q.second;
             int64_t m = f.p % f.q;
@@ -1308,7 +1466,7 @@ struct Lower {
     bool same_irr(const Kd& a, const Kd& b) const {
         const auto ia = irr(a.sig), ib = irr(b.sig);
         if (ia.empty() || ia.size() != ib.size()) return false;
-        std::vector<bool> used(ib.size(), false);
+        TVec<bool> used(ib.size(), false);
         for (const auto& p : ia) {
             bool ok = false;
             for (size_t k = 0; k < ib.size(); ++k)
@@ -1337,10 +1495,10 @@ struct Lower {
                     return Kd{3, {e}, true, mksig({{x.a, e}})};
                 }
                 if (k.t == 3 && k.pure) {
-                    std::vector<Rat> ex;
+                    TVec<Rat> ex;
                     for (Rat a : k.ex) { Rat m = rmul(a, e); if (!rint(m)) ex.push_back(m); }
                     if (ex.empty()) return Kd{1, {}, false};
-                    std::vector<std::pair<int, Rat>> sg;
+                    TVec<std::pair<int, Rat>> sg;
                     for (const auto& q : k.sig) sg.push_back({q.first, rmul(q.second, e)});
                     return Kd{3, ex, true, mksig(sg)};
                 }
@@ -1359,7 +1517,7 @@ struct Lower {
         if (x.k == IADD || x.k == ISUB) {
             if (ka.t == kb.t && (ka.t == 1 || ka.t == 2)) return Kd{ka.t, {}, false};
             if (ka.t == 3 && kb.t == 3 && same_irr(ka, kb)) {   // r1*H + r2*H = (r1 + r2)*H
-                std::vector<Rat> ex = ka.ex;
+                TVec<Rat> ex = ka.ex;
                 ex.insert(ex.end(), kb.ex.begin(), kb.ex.end());
                 return Kd{3, ex, false, ka.sig};
             }
@@ -1370,8 +1528,8 @@ struct Lower {
         }
         if (ka.t == 0 || kb.t == 0 || ka.t == 2 || kb.t == 2) return Kd{0, {}, false};
         if (ka.t == 1 && kb.t == 1) return Kd{1, {}, false};
-        std::vector<Rat> ex = ka.t == 3 ? ka.ex : std::vector<Rat>{};
-        std::vector<std::pair<int, Rat>> sg = ka.t == 3 ? ka.sig : std::vector<std::pair<int, Rat>>{};
+        TVec<Rat> ex = ka.t == 3 ? ka.ex : TVec<Rat>{};
+        TVec<std::pair<int, Rat>> sg = ka.t == 3 ? ka.sig : TVec<std::pair<int, Rat>>{};
         if (kb.t == 3) {
             for (Rat r : kb.ex) ex.push_back(x.k == IDIV ? rneg(r) : r);
             for (const auto& q : kb.sig) sg.push_back({q.first, x.k == IDIV ? rneg(q.second) : q.second});
@@ -1512,6 +1670,7 @@ bool is_p_op(int o) { return o >= PDOP_PUSH_P && o <= PDOP_RDIV_P; }
 int compile_one(Ctx& C, const SymInfo* syms, int nsyms, const char* s, size_t len,
                 std::vector<int32_t>& out, std::string* canon) {
     try {
+        g_arena.rewind();
         C.reset(syms, nsyms);
         Parser P(C, s, len);
         const int root = P.parse();
