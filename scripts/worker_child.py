@@ -6,7 +6,7 @@ validated force-free d4 stream and runs the worker's pipeline (pdeval.worker.pro
 over them.
 
 Protocol: prints READY once its context, SymPy pool and tagger are warm; waits for one line
-on stdin; then prints one JSON line {rows, seconds, digest} where digest is the SHA-256 of the
+on stdin; then prints one JSON line {rows, seconds, t0, t1, digest} where digest is the SHA-256 of the
 repr of its result tuples, batch by batch in its own order (over all --passes), computed after
 the timed region."""
 import argparse
@@ -55,7 +55,9 @@ def main():
     h = hashlib.sha256()
     for r in got:
         h.update(repr(r).encode())
-    print(json.dumps({'rows': n, 'seconds': dt, 'digest': h.hexdigest()}), flush=True)
+    # t0 / t1: time.perf_counter() (CLOCK_MONOTONIC, one clock for every process of the box), so
+    # the parent times the pool from the first start to the last end, without this digest
+    print(json.dumps({'rows': n, 'seconds': dt, 't0': t0, 't1': t0 + dt, 'digest': h.hexdigest()}), flush=True)
     hostpool.stop()
 
 

@@ -3,7 +3,7 @@
 each taking every N-th 4,096-row queue batch of the validated force-free d4 strings) under
 host-thread settings: PDEVAL_HOST_THREADS (native compile threads per call) and the pipeline's
 compile threads / depth (PDEVAL_PIPE_COMPILERS, PDEVAL_PIPE_DEPTH).  One JSON line per setting.
-GPU box only.  Usage: python scripts/worker_pool_sweep.py"""
+GPU box only.  Usage: python scripts/worker_pool_sweep.py [--procs 2,3,4]"""
 import json
 import os
 import sys
@@ -29,6 +29,13 @@ def main():
                 ({'PDEVAL_HOST_THREADS': '4', 'PDEVAL_PIPE_COMPILERS': '2'}, 2),
                 ({'PDEVAL_HOST_THREADS': '8', 'PDEVAL_PIPE_DEPTH': '12'}, 2),
                 ({'PDEVAL_HOST_THREADS': '4'}, 3), ({'PDEVAL_HOST_THREADS': '4'}, 4)]
+    if '--pipe' in sys.argv:      # pipeline shapes at 2 processes
+        settings = [({}, 2), ({'PDEVAL_PIPE_DEPTH': '16', 'PDEVAL_PIPE_COMPILERS': '8'}, 2),
+                    ({'PDEVAL_PIPE_DEPTH': '16', 'PDEVAL_PIPE_COMPILERS': '8', 'PDEVAL_HOST_THREADS': '8'}, 2),
+                    ({'PDEVAL_PIPE_DEPTH': '12', 'PDEVAL_PIPE_COMPILERS': '6'}, 2),
+                    ({'PDEVAL_PIPE_DEPTH': '16', 'PDEVAL_PIPE_COMPILERS': '8'}, 3)]
+    if '--procs' in sys.argv:     # only the default host settings, at these process counts
+        settings = [({}, int(k)) for k in sys.argv[sys.argv.index('--procs') + 1].split(',')]
     for env, procs in settings:
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
