@@ -896,13 +896,15 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 }
 
 // waves per SIMD of pass 1: force-free 5 (96 VGPRs with the x power table, 48 B of spill;
-// 4 waves 149.3 vs 146.9 ms, profiles/r04_c_*), Kerr 6 (80 VGPRs with the late coefficient
+// 4 waves 149.3 vs 146.9 ms, profiles/r04_c_*), Kerr 6 at W = 2 (80 VGPRs with the late coefficient
 // loads; 5: 49.0 ms, 6: 46.5)
 #ifndef PD_GRID_WAVES_PER_SIMD
 #define PD_GRID_WAVES_PER_SIMD 5
 #endif
+// Kerr pass 1 at W = 3 rows per dispatch (below): 94 VGPRs, 5 waves/SIMD, no spill (W = 2 at 6
+// waves: 48.6 ms per 2^21 step; W = 3 at 5: 47.1-47.5; W = 4 at 4: 47.6-47.8, profiles/r06_s_*)
 #ifndef PD_KERR_WAVES_PER_SIMD
-#define PD_KERR_WAVES_PER_SIMD 6
+#define PD_KERR_WAVES_PER_SIMD 5
 #endif
 // Kerr pass 1 loads the operator coefficients after the interpreter: 16 fewer VGPRs live
 // through it, so 6 waves/SIMD fit without spilling (80 VGPRs): pass 1 48.6 -> 46.5 ms
@@ -917,7 +919,7 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 #define PD_LIST_WAVES_PER_SIMD 4
 #endif
 #ifndef PD_KERR_W
-#define PD_KERR_W 2
+#define PD_KERR_W 3
 #endif
 #ifndef PD_DEEP_W
 #define PD_DEEP_W 2
@@ -930,7 +932,8 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 // Folding stack 3 into pass 1 (a runtime slot index, and two slots of LDS per wave for every
 // candidate) measured slower for Kerr: 66.1 ms against 49.9 + 13.5 ms (d<=3 batch).
 // W = grid rows per dispatch (Lean above): 1 for force-free, PD_KERR_W for Kerr in pass 1,
-// PD_DEEP_W for Kerr in pass 2; an odd last row runs alone.
+// PD_DEEP_W for Kerr in pass 2; the rows of a last, partial group past nx are evaluated (their
+// x clamped to the last row) and skipped by the epilogue (64 rows at W = 3: 22 groups, 2 spare).
 template <int PROB, int MAXD> constexpr int grid_w() {
     return PROB == PDEVAL_PROBLEM_FORCE_FREE ? 1 : (MAXD == 2 ? PD_KERR_W : PD_DEEP_W);
 }
