@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 6, session w: Kerr pass 2 at W = 1 (115 VGPRs, no spill, 4 waves/SIMD) against the
+# shipped W = 2 (128 VGPRs + 96 B spill), alternated twice.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=r06_w
+for k in 1 2; do
+  for v in "" _kd1s4; do
+    PDEVAL_LIB=pde-engine_amd/lib/libpdeval$v.so timeout -k 10 300 python bench.py --problem kerr_magnetosphere --no-cpu --no-extras --steps 5 > gpurun_out/${T}_kerr${v}_$k.log 2>&1 || exit 7
+  done
+done
+echo ALL_RC=0
