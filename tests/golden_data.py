@@ -155,9 +155,13 @@ def ff_d5f_files():
 # by tests/golden/score_d5f.py with pdeval.symbolic.suspect frozen at commit 5708cbc, held out:
 # the rule was not refitted): functions of rho/z, det == 0 identically, that the reference's
 # symbolic stage cannot reduce (its false negatives) ...
-FF_D5F_OFF_DIVERGENCE = frozenset({'2*rho/z - pow_3_2(sqrt(rho/z))', 'rho/z - pow_3_2(sqrt(neg(rho/z)))'})
-# ... of which the frozen suspect rule flags the first (strict replays it and agrees), not the
-# second (a radical of neg(rho/z): strict keeps the device's accept)
+FF_D5F_OFF_DIVERGENCE = frozenset({'2*rho/z - pow_3_2(sqrt(rho/z))', 'rho/z - pow_3_2(sqrt(neg(rho/z)))',
+                                   # (rows 4,000-6,350 of the sample, scored after they were
+                                   # drawn, the rule still frozen: the same family)
+                                   '(rho/z)**(1/4) + z/rho', '-inv(rho/z) + pow_neg_3_2(sqrt(rho/z))'})
+# ... of which the frozen suspect rule flags all but 'rho/z - pow_3_2(sqrt(neg(rho/z)))' (strict
+# replays them and agrees); that one, a radical of neg(rho/z), it does not flag: strict keeps the
+# device's accept
 FF_D5F_STRICT_DIVERGENCE = frozenset({'rho/z - pow_3_2(sqrt(neg(rho/z)))'})
 FF_D5_SYMBOLIC_DIVERGENCE = {'exp_neg(rho/z - sqrt(rho/z))'}
 # Every decided force-free fixture row on which the default mode ('off': the grid's det == 0

@@ -669,8 +669,9 @@ def test_plugin_api_depth5_faithful():
     """configs[3]'s depth on the reference's OWN depth-5 distribution: the
     faithful sample's decided rows (G.ff_d5f_files(); the suspect rule frozen before the sample
     was drawn) through the plugin on the GPU, default mode: every verdict equals the
-    reference's except the rows G.FF_D5F_OFF_DIVERGENCE lists (none); reason texts are
-    reported."""
+    reference's except the rows G.FF_D5F_OFF_DIVERGENCE lists (4 of 2,066 decided rows, all
+    functions of rho/z whose det == 0 the reference's symbolic stage does not reduce); reason
+    texts are reported."""
     from problems import load_problem
     import sympy as sp
     files = G.ff_d5f_files()
