@@ -6,9 +6,16 @@ The depth-5 stream (configs[3]) is not enumerable here (~12.4 M candidates to no
 grammar instead: one more operation on top of the depth-4 candidates that reach ``validate``
 (``streams/force_free_d4_validated.txt.gz``) --
   * a unary op of the problem (``expression_operations.UNARY_OPS``) on a depth-4 candidate;
-  * a binary op (``BINARY_OPS``) of a depth-4 candidate and a depth <= 1 one
-    (``rho``, ``z``, and the unary ops applied to them) -- the enumerator's depth rule
-    (``lean_bridge_fixed.py:113-215``: depth(op(a, b)) = 1 + max(depth a, depth b)).
+  * a binary op (``BINARY_OPS``) of a depth-4 candidate and a "leaf" (``rho``, ``z``, and the
+    unary ops applied to them).
+This is a PROXY grammar, not the enumerator's: its binary depth is additive
+(``lean_bridge_fixed.py:155-157``: ``for d1 in range(1, depth): d2 = depth - d1``, so depth 5
+pairs (1,4), (2,3), (3,2), (4,1)), its depth-1 set is the five primitives
+``rho, z, rho**2 + z**2, rho/z, 1`` (``problems/__init__.py:73-79``), its splices are
+unparenthesised (``:166-195``), and its candidates go through ``normalize_batch``, the signature
+dedupe and the pre-validate filters -- so part of this sample is depth 6 (a unary leaf is depth 2)
+and the (2,3)/(3,2) pairs are absent.  The faithful sample is ``gen_d5_faithful.py``; this one
+stays as a further stress set of the same vocabulary (``ref/ff_d5_s*.jsonl``).
 Strings are written as the stream writes them: unary ops by name (``sqrt(<a>)``; the driver's
 ``sympify`` locals hold the unary ops, ``general_method_paper_reproduction.py:1703-1712``) and
 binary ops as SymPy infix (``geom_sum(a, b)`` = ``a/(1 - b)``, ``expression_operations.py``).  Output: ``tests/golden/streams/force_free_d5_sample.txt.gz`` ("5\\t<expr>" per line),
