@@ -426,8 +426,11 @@ __global__ __launch_bounds__(256) void ptab_kernel(const double* gx, const doubl
 #ifndef PD_PTAB
 #define PD_PTAB 2
 #endif
+// Kerr at W = 3 rows per dispatch: no tables (the x powers formed in place, no scalar loads of
+// the table per opcode) 47.4 -> 46.6 ms for pass 1, three alternations on one box, classes
+// identical (profiles/r06_ae_*; x table only was the round-4 choice at W = 2)
 #ifndef PD_PTAB_KERR
-#define PD_PTAB_KERR 2
+#define PD_PTAB_KERR 0
 #endif
 // Where a lane finds its coordinate-power coefficients: x rows px[q] (wave-uniform), the
 // lane's ordinate py; strides per n: sx (x part), sy (y part), and ny between coefficients.
