@@ -924,11 +924,12 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 #ifndef PD_KERR_W
 #define PD_KERR_W 3
 #endif
-// Kerr pass 2 (the stack-3 list) at W = 3 rows per dispatch, 4 waves/SIMD (128 VGPRs + 128 B/lane
-// of spill): 19.8 -> 18.0 ms per 2^21 step against W = 2 (96 B spill); W = 1 27.4 ms, W = 3 at 3
-// waves 20.9, W = 4 at 3 waves 19.0 (profiles/r06_t_*, r06_w_*, r06_w2_*)
+// Kerr pass 2 (the stack-3 list) at W = 4 rows per dispatch, 4 waves/SIMD (128 VGPRs + 192 B/lane
+// of spill): W = 2 (96 B spill) 19.8 ms per 2^21 step, W = 3 18.0, W = 4 17.4 (without the power
+// tables, three alternations); W = 1 27.4 ms, W = 3 at 3 waves 20.9, W = 4 at 3 waves 19.0
+// (profiles/r06_t_*, r06_w_*, r06_w2_*, r06_ah_*)
 #ifndef PD_DEEP_W
-#define PD_DEEP_W 3
+#define PD_DEEP_W 4
 #endif
 // Two lean passes share one body (grid_body):
 //   pass 1  grid_kernel       every candidate, one wave each (256-thread blocks), stack <= 2
