@@ -926,8 +926,9 @@ __device__ __forceinline__ void grid_finish(const KernelArgs& a, int64_t cand, u
 #endif
 // Kerr pass 2 (the stack-3 list) at W = 4 rows per dispatch, 4 waves/SIMD (128 VGPRs + 192 B/lane
 // of spill): W = 2 (96 B spill) 19.8 ms per 2^21 step, W = 3 18.0, W = 4 17.4 (without the power
-// tables, three alternations); W = 1 27.4 ms, W = 3 at 3 waves 20.9, W = 4 at 3 waves 19.0
-// (profiles/r06_t_*, r06_w_*, r06_w2_*, r06_ah_*)
+// tables, three alternations); W = 1 27.4 ms, W = 3 at 3 waves 20.9, W = 4 at 3 waves 19.0, W = 5
+// 21.7 and W = 6 29.9 (their LDS operand slots cap the waves per CU) (profiles/r06_t_*, r06_w_*,
+// r06_w2_*, r06_ah_*, r06_aj_*)
 #ifndef PD_DEEP_W
 #define PD_DEEP_W 4
 #endif
